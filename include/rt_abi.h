@@ -1,0 +1,159 @@
+/* rt_abi.h — C-ABI of the MI355X path tracer (librtamd.so, HIP for gfx950).
+ *
+ * Drop-in replacement for the reference's OpenGL program interface of the path-tracing
+ * fragment shader (src/shaders/fragment_shader_ray_tracing.glsl, "RT:"), which the
+ * reference drives from src/sources/main.cpp.  Entry point -> reference interface:
+ *
+ *   rt_create / rt_destroy   <- Shader RayTracerShader(...) + GL context (src/core/Shader.h:21-108,
+ *                               main.cpp:93-95)
+ *   rt_set_scene             <- EncodedBVHandTriangles() glBufferData/glTexBuffer uploads of the
+ *                               triangle and BVH texture buffers (src/core/Scene.h:240-256) and the
+ *                               nTriangles/nNodes uniforms (main.cpp:135-136); SoA instead of AoS
+ *   rt_set_scene_encoded     <- the same upload taking the reference's AoS encodings verbatim
+ *                               (Triangle_encoded src/core/Triangle.h:28-39, BVHNode_encoded
+ *                               src/core/BVH.h:17-21)
+ *   rt_update_materials      <- RefreshTriangleMaterial re-upload (src/core/Triangle.h:133-151),
+ *                               with post-BVH triangle indices
+ *   rt_set_env               <- InitHdrEnvMap() hdrMap/hdrCache RGB32F textures + hdrResolution
+ *                               (src/core/Scene.h:164-184, main.cpp:138, :149-155)
+ *   rt_resize                <- RenderBuffer::Init/Resize RGB32F ping-pong FBOs (src/core/Screen.h:110-122)
+ *                               + this rank's pixel tiles (multi-GPU sharding, new)
+ *   rt_reset / rt_set_loop_num <- camera.LoopNum = 0 (main.cpp:326, src/core/Camera.h:453)
+ *   rt_render(_async)        <- per-frame loop body main.cpp:175-200: LoopIncrease, setCurrentBuffer,
+ *                               the uniform list of main.cpp:181-199, DrawScreen
+ *   rt_read_accum            <- reading the accumulation texture (Utility.h:19-30 SaveFrame reads it
+ *                               after tone mapping; here the raw fp32 history)
+ *   rt_accum_device / rt_assemble_frame <- (new) device-side tile gather for RCCL
+ *
+ * Conventions: every function returns RT_OK (0) or a negative rt_err_*; nothing aborts.
+ * A context is bound to one HIP device and is not thread-safe (one host thread per ctx),
+ * matching the single GL context of the reference (main.cpp:72).
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  RT_OK = 0,
+  RT_ERR_ARG = -1,
+  RT_ERR_HIP = -2,      /* a HIP runtime call failed; rt_last_error() has the text */
+  RT_ERR_STATE = -3,    /* call order (e.g. render before set_scene/resize)          */
+  RT_ERR_NOMEM = -4,
+  RT_ERR_NODEVICE = -5, /* no HIP device / bad ordinal                               */
+  RT_ERR_LIMIT = -6     /* scene exceeds a kernel limit (leaf > 16 tris, depth > 64) */
+};
+
+enum { RT_MAX_FRAMES_PER_LAUNCH = 64 };
+
+/* Disney material (src/core/Material.h:25-46), 24 floats, same layout as rts_material. */
+typedef struct rt_material {
+  float emissive[3];
+  float base_color[3];
+  float subsurface, metallic, specular, specular_tint, roughness, anisotropic;
+  float sheen, sheen_tint, clearcoat, clearcoat_gloss, ior, transmission;
+  float medium_color[3];
+  float medium_type, medium_density, medium_anisotropy;
+} rt_material;
+
+/* Scene in post-BVH triangle order (what buildBVHwithSAH leaves in `triangles`). */
+typedef struct rt_scene_soa {
+  int32_t n_triangles;
+  const float *p1, *p2, *p3;      /* float[3*n_triangles], xyz interleaved */
+  const float *n1, *n2, *n3;      /* vertex normals, float[3*n_triangles]  */
+  const int32_t* material_id;     /* [n_triangles] index into materials    */
+  const rt_material* materials;
+  int32_t n_materials;
+  int32_t n_nodes;                /* reference numbering: node 0 dummy, root 1, child 0 = none */
+  const int32_t *node_left, *node_right, *node_n, *node_index;
+  const float *node_aa, *node_bb; /* float[3*n_nodes] */
+} rt_scene_soa;
+
+/* Pixel tiling: the frame is cut into tile_w x tile_h tiles (multiples of 8), numbered
+ * row-major from the bottom-left; this context renders tiles t with t % world == rank. */
+typedef struct rt_tiling {
+  int32_t tile_w, tile_h, rank, world;
+} rt_tiling;
+
+/* Per-call uniforms (main.cpp:181-199).  screen size comes from rt_resize. */
+typedef struct rt_frame_params {
+  float position[3], front[3], right[3], up[3], left_bottom_corner[3];
+  float half_h, half_w;
+  int32_t enable_mis, enable_env_map, enable_bsdf;
+  float env_intensity, env_angle;
+  int32_t max_bounce, max_iterations;
+  int32_t flags;                  /* RT_FLAG_* */
+} rt_frame_params;
+
+enum {
+  RT_FLAG_NO_CULL = 1,            /* disable closest-hit box culling (exhaustive RT:338 order)  */
+  RT_FLAG_COUNT_VISITS = 2        /* also count node/triangle visits (slower)                  */
+};
+
+typedef struct rt_stats {
+  uint64_t rays;            /* hitBVH invocations: camera + NEE shadow + continuation    */
+  uint64_t samples;         /* pixel samples traced (frames x pixels, R12 copies excluded) */
+  uint64_t internal_pops, leaf_pops, tri_tests;  /* only with RT_FLAG_COUNT_VISITS */
+  uint64_t launches;
+  double kernel_ms;         /* sum of kernel durations (HIP events) since rt_stats_reset  */
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+
+int rt_create(int hip_device, rt_ctx** out);
+int rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+/* Device properties used for the launch geometry (CUs, clock). */
+int rt_device_info(const rt_ctx* ctx, int32_t* n_cus, int32_t* blocks_per_cu, int32_t* lds_bytes_per_block);
+
+int rt_set_scene(rt_ctx* ctx, const rt_scene_soa* scene);
+int rt_set_scene_encoded(rt_ctx* ctx, const float* tri_enc, int32_t n_triangles, const float* node_enc,
+                         int32_t n_nodes);
+int rt_update_materials(rt_ctx* ctx, int32_t first, int32_t count, const rt_material* material);
+/* hdr_rgb / cache_rgb: w*h*3 floats, row 0 = first uploaded row (texture v = 0). */
+int rt_set_env(rt_ctx* ctx, const float* hdr_rgb, const float* cache_rgb, int32_t w, int32_t h,
+               int32_t hdr_resolution);
+int rt_resize(rt_ctx* ctx, int32_t width, int32_t height, const rt_tiling* tiling /* NULL = whole frame */);
+int rt_reset(rt_ctx* ctx);                       /* LoopNum = 0 (history kept, as the FBOs are) */
+int rt_set_loop_num(rt_ctx* ctx, int32_t loop_num);
+int rt_get_loop_num(const rt_ctx* ctx, int32_t* loop_num);
+/* Clear this rank's accumulation to zero (fresh FBO contents). */
+int rt_clear_accum(rt_ctx* ctx);
+
+/* Enqueue n_frames progressive frames (one randOrigin per frame) on the ctx stream.  Each
+ * frame first applies main.cpp:175 (LoopNum++ unless it reached max_iterations). */
+int rt_render_async(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames);
+/* rt_render_async + synchronise + optional stats snapshot. */
+int rt_render(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
+              rt_stats* stats);
+int rt_synchronize(rt_ctx* ctx);
+int rt_stats_get(rt_ctx* ctx, rt_stats* stats);  /* synchronises */
+int rt_stats_reset(rt_ctx* ctx);
+
+/* The HIP stream (hipStream_t) the ctx launches on, for external events / collectives. */
+int rt_get_stream(const rt_ctx* ctx, void** stream);
+int rt_set_stream(rt_ctx* ctx, void* stream /* NULL = ctx-owned stream */);
+
+enum { RT_LAYOUT_FRAME = 0, RT_LAYOUT_LOCAL_TILES = 1 };
+/* FRAME: rgb_out = width*height*3 floats, row 0 = bottom row (GL framebuffer order); only this
+ * rank's pixels are written.  LOCAL_TILES: local_tiles*tile_h*tile_w*3 floats. */
+int rt_read_accum(rt_ctx* ctx, float* rgb_out, int32_t layout);
+/* Upload a history (same layouts) — e.g. resume from a saved accumulation. */
+int rt_write_accum(rt_ctx* ctx, const float* rgb_in, int32_t layout);
+/* Device accumulation buffer: float4 (rgb + pad) per local tile pixel, padded to
+ * max_local_tiles tiles so that every rank's buffer has the same size. */
+int rt_accum_device(const rt_ctx* ctx, void** device_ptr, size_t* bytes, int32_t* local_tiles,
+                    int32_t* max_local_tiles);
+/* Un-permute `world` gathered accumulation buffers (rank-major, each rt_accum_device bytes) on
+ * this ctx's device into a width*height*3 float frame (device pointer). */
+int rt_assemble_frame(rt_ctx* ctx, const void* gathered_device, int32_t world, void* frame_device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,577 @@
+// rt_render.hip — librtamd.so: the C-ABI of include/rt_abi.h over the gfx950 path-tracing
+// kernels of rt_kernels.h.  Host code here converts the reference's scene description
+// (SoA or the reference's own AoS encodings) into the device layout, owns the device
+// buffers and launches the persistent kernel.  No fallback path: without a HIP device every
+// entry point returns RT_ERR_NODEVICE / RT_ERR_HIP.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_kernels.h"
+
+using rtd::GNode;
+using rtd::KParams;
+
+struct rt_ctx {
+  int device = 0;
+  int n_cus = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // scene
+  GNode* d_nodes = nullptr;
+  float4* d_tri = nullptr;
+  float4* d_trin = nullptr;
+  float4* d_mats = nullptr;
+  int n_tri = 0, n_mats = 0, root = 0, has_scene = 0, stack_entries = 2;
+  bool scene_set = false;
+  std::vector<int32_t> tri_mat;  // host copy of the per-triangle material ids (for updates)
+  std::vector<float> mat_table;  // host copy, 32 floats per material
+  // env
+  float4* d_hdr = nullptr;
+  float4* d_cache = nullptr;
+  int hdr_w = 0, hdr_h = 0, hdr_res = 0;
+  bool env_set = false;
+  // frame
+  int W = 0, H = 0, tile_w = 32, tile_h = 32, tiles_x = 0, tiles_y = 0, rank = 0, world = 1;
+  int local_tiles = 0, max_local_tiles = 0;
+  float4* d_accum = nullptr;
+  bool frame_set = false;
+  int loop_num = 0;
+  // counters
+  unsigned int* d_counter = nullptr;
+  unsigned long long* d_stats = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  double kernel_ms = 0.0;
+  uint64_t launches = 0;
+  int blocks_per_cu = 0, block_lds = 0;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(ctx, call)                                                                        \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail((ctx), RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));         \
+  } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+// Same fp32 operations as the shader's per-test N = normalize(cross(p2-p1, p3-p1)) (RT:253).
+inline void geometric_normal(const float* p1, const float* p2, const float* p3, float* n) {
+  float ax = p2[0] - p1[0], ay = p2[1] - p1[1], az = p2[2] - p1[2];
+  float bx = p3[0] - p1[0], by = p3[1] - p1[1], bz = p3[2] - p1[2];
+  float cx = ay * bz - by * az, cy = az * bx - bz * ax, cz = ax * by - bx * ay;
+  float inv = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);
+  n[0] = cx * inv; n[1] = cy * inv; n[2] = cz * inv;
+}
+
+// Material.h fields -> 32-float device entry; ax/ay by getMaterial's formula (RT:205-207).
+void pack_material(const rt_material& m, float* o) {
+  const float* f = reinterpret_cast<const float*>(&m);
+  for (int k = 0; k < 24; k++) o[k] = f[k];
+  float aspect = gm::sqrt_(1.0f - m.anisotropic * 0.9f);
+  o[24] = gm::max_(0.001f, (m.roughness * m.roughness) / aspect);
+  o[25] = gm::max_(0.001f, (m.roughness * m.roughness) * aspect);
+  int mt = (int)m.medium_type;
+  memcpy(&o[26], &mt, 4);
+  o[27] = o[28] = o[29] = o[30] = o[31] = 0.0f;
+}
+
+int upload(rt_ctx* c, void** dst, const void* src, size_t bytes) {
+  if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
+  if (bytes == 0) return RT_OK;
+  HIPCHK(c, hipMalloc(dst, bytes));
+  HIPCHK(c, hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+int occupancy(rt_ctx* c) {
+  int lds = c->stack_entries * 256 * 8;
+  int bpc = 0;
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::rt_path_kernel<false>, 256, lds));
+  if (bpc < 1) bpc = 1;
+  c->blocks_per_cu = bpc;
+  c->block_lds = lds;
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_create(int hip_device, rt_ctx** out) {
+  if (!out) return RT_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_NODEVICE;
+  if (hip_device < 0 || hip_device >= n) return RT_ERR_NODEVICE;
+  rt_ctx* c = new (std::nothrow) rt_ctx();
+  if (!c) return RT_ERR_NOMEM;
+  c->device = hip_device;
+  if (hipSetDevice(hip_device) != hipSuccess) { delete c; return RT_ERR_HIP; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) { delete c; return RT_ERR_HIP; }
+  c->n_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
+  c->own_stream = true;
+  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    rt_destroy(c);
+    return RT_ERR_HIP;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+  if (!c) return RT_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  dfree(c->d_nodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
+  dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int rt_device_info(const rt_ctx* c, int32_t* n_cus, int32_t* blocks_per_cu, int32_t* lds_bytes_per_block) {
+  if (!c) return RT_ERR_ARG;
+  if (n_cus) *n_cus = c->n_cus;
+  if (blocks_per_cu) *blocks_per_cu = c->blocks_per_cu;
+  if (lds_bytes_per_block) *lds_bytes_per_block = c->block_lds;
+  return RT_OK;
+}
+
+int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
+  if (!c || !s) return RT_ERR_ARG;
+  if (s->n_triangles < 0 || s->n_nodes < 0 || s->n_materials < 0) return fail(c, RT_ERR_ARG, "negative count");
+  const int nt = s->n_triangles;
+  if (nt > 0 && (!s->p1 || !s->p2 || !s->p3 || !s->n1 || !s->n2 || !s->n3 || !s->material_id || !s->materials))
+    return fail(c, RT_ERR_ARG, "missing triangle arrays");
+  if (nt >= (1 << 27)) return fail(c, RT_ERR_LIMIT, "more than 2^27 triangles");
+  HIPCHK(c, hipSetDevice(c->device));
+  for (int i = 0; i < nt; i++)
+    if (s->material_id[i] < 0 || s->material_id[i] >= s->n_materials)
+      return fail(c, RT_ERR_ARG, "material_id out of range");
+  // ---- triangles
+  std::vector<float4> tri(3 * (size_t)nt), trin(3 * (size_t)nt);
+  for (int i = 0; i < nt; i++) {
+    float ng[3];
+    geometric_normal(s->p1 + 3 * i, s->p2 + 3 * i, s->p3 + 3 * i, ng);
+    const float* ps[3] = {s->p1 + 3 * i, s->p2 + 3 * i, s->p3 + 3 * i};
+    const float* ns[3] = {s->n1 + 3 * i, s->n2 + 3 * i, s->n3 + 3 * i};
+    for (int k = 0; k < 3; k++) {
+      tri[3 * i + k] = make_float4(ps[k][0], ps[k][1], ps[k][2], ng[k]);
+      float w = 0.0f;
+      if (k == 0) memcpy(&w, &s->material_id[i], 4);
+      trin[3 * i + k] = make_float4(ns[k][0], ns[k][1], ns[k][2], w);
+    }
+  }
+  // ---- materials
+  std::vector<float> mt(32 * (size_t)std::max(1, s->n_materials), 0.0f);
+  for (int m = 0; m < s->n_materials; m++) pack_material(s->materials[m], &mt[32 * m]);
+  // ---- BVH: reference numbering -> children-in-parent nodes
+  int root = 0, has = 0, depth = 1;
+  std::vector<GNode> gn;
+  if (nt > 0 && s->n_nodes > 1) {
+    if (!s->node_left || !s->node_right || !s->node_n || !s->node_index || !s->node_aa || !s->node_bb)
+      return fail(c, RT_ERR_ARG, "missing node arrays");
+    const int nn = s->n_nodes;
+    std::vector<int> internal_id(nn, -1);
+    auto is_leaf = [&](int i) { return s->node_n[i] > 0; };
+    auto leaf_ref = [&](int i, int& ref) -> int {
+      int n = s->node_n[i], first = s->node_index[i];
+      if (n > 16) return fail(c, RT_ERR_LIMIT, "leaf with more than 16 triangles");
+      if (first < 0 || first + n > nt) return fail(c, RT_ERR_ARG, "leaf range outside the triangle list");
+      ref = (int)(rtd::LEAF_BIT | ((uint32_t)first << 4) | (uint32_t)(n - 1));
+      return RT_OK;
+    };
+    // DFS from the root (node 1) assigning internal ids, checking structure and depth
+    std::vector<std::pair<int, int>> st;
+    st.push_back({1, 1});
+    std::vector<int> order;
+    while (!st.empty()) {
+      auto e = st.back();
+      st.pop_back();
+      int i = e.first;
+      if (i <= 0 || i >= nn) return fail(c, RT_ERR_ARG, "child index out of range");
+      depth = std::max(depth, e.second);
+      if (depth > 64) return fail(c, RT_ERR_LIMIT, "BVH deeper than 64 levels");
+      if (is_leaf(i)) continue;
+      if (internal_id[i] >= 0) return fail(c, RT_ERR_ARG, "BVH is not a tree");
+      if (s->node_left[i] <= 0 || s->node_right[i] <= 0) return fail(c, RT_ERR_ARG, "internal node without two children");
+      internal_id[i] = (int)order.size();
+      order.push_back(i);
+      st.push_back({s->node_right[i], e.second + 1});
+      st.push_back({s->node_left[i], e.second + 1});
+    }
+    gn.resize(std::max<size_t>(1, order.size()));
+    for (size_t k = 0; k < order.size(); k++) {
+      int i = order[k];
+      int l = s->node_left[i], r = s->node_right[i];
+      const float* la = s->node_aa + 3 * l; const float* lb = s->node_bb + 3 * l;
+      const float* ra = s->node_aa + 3 * r; const float* rb = s->node_bb + 3 * r;
+      GNode g;
+      g.b0 = make_float4(la[0], la[1], la[2], lb[0]);
+      g.b1 = make_float4(lb[1], lb[2], ra[0], ra[1]);
+      g.b2 = make_float4(ra[2], rb[0], rb[1], rb[2]);
+      int lr, rr;
+      int rc;
+      if (is_leaf(l)) { if ((rc = leaf_ref(l, lr))) return rc; } else lr = internal_id[l];
+      if (is_leaf(r)) { if ((rc = leaf_ref(r, rr))) return rc; } else rr = internal_id[r];
+      g.ref = make_int4(lr, rr, 0, 0);
+      gn[k] = g;
+    }
+    if (is_leaf(1)) {
+      int rc = leaf_ref(1, root);
+      if (rc) return rc;
+    } else {
+      root = internal_id[1];
+    }
+    has = 1;
+  }
+  if (gn.empty()) {
+    GNode z;
+    memset(&z, 0, sizeof(z));
+    gn.push_back(z);
+  }
+  int rc;
+  if ((rc = upload(c, (void**)&c->d_nodes, gn.data(), gn.size() * sizeof(GNode)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_tri, tri.data(), tri.size() * sizeof(float4)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_trin, trin.data(), trin.size() * sizeof(float4)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_mats, mt.data(), mt.size() * sizeof(float)))) return rc;
+  c->n_tri = nt;
+  c->n_mats = s->n_materials;
+  c->root = root;
+  c->has_scene = has;
+  c->stack_entries = std::max(2, depth + 1);
+  c->tri_mat.assign(s->material_id, s->material_id + nt);
+  c->mat_table = mt;
+  c->scene_set = true;
+  return occupancy(c);
+}
+
+int rt_set_scene_encoded(rt_ctx* c, const float* tri_enc, int32_t n_triangles, const float* node_enc, int32_t n_nodes) {
+  if (!c || n_triangles < 0 || n_nodes < 0 || (n_triangles && !tri_enc) || (n_nodes && !node_enc)) return RT_ERR_ARG;
+  const size_t nt = (size_t)n_triangles;
+  std::vector<float> p[6];
+  for (auto& v : p) v.resize(3 * nt);
+  std::vector<int32_t> mid(nt);
+  std::vector<rt_material> mats;
+  for (size_t i = 0; i < nt; i++) {
+    const float* t = tri_enc + 42 * i;  // Triangle_encoded: 14 texels
+    for (int k = 0; k < 6; k++) memcpy(&p[k][3 * i], t + 3 * k, 12);
+    rt_material m;
+    memcpy(&m, t + 18, sizeof(rt_material));
+    int found = -1;
+    for (size_t q = 0; q < mats.size(); q++)
+      if (!memcmp(&mats[q], &m, sizeof(m))) { found = (int)q; break; }
+    if (found < 0) { mats.push_back(m); found = (int)mats.size() - 1; }
+    mid[i] = found;
+  }
+  std::vector<int32_t> L(n_nodes), R(n_nodes), N(n_nodes), I(n_nodes);
+  std::vector<float> aa(3 * (size_t)n_nodes), bb(3 * (size_t)n_nodes);
+  for (int i = 0; i < n_nodes; i++) {  // BVHNode_encoded: ints stored as floats (RT:224-230 casts)
+    const float* nd = node_enc + 12 * (size_t)i;
+    L[i] = (int)nd[0]; R[i] = (int)nd[1]; N[i] = (int)nd[3]; I[i] = (int)nd[4];
+    memcpy(&aa[3 * i], nd + 6, 12);
+    memcpy(&bb[3 * i], nd + 9, 12);
+  }
+  rt_scene_soa s;
+  s.n_triangles = n_triangles;
+  s.p1 = p[0].data(); s.p2 = p[1].data(); s.p3 = p[2].data();
+  s.n1 = p[3].data(); s.n2 = p[4].data(); s.n3 = p[5].data();
+  s.material_id = mid.data();
+  s.materials = mats.data();
+  s.n_materials = (int32_t)mats.size();
+  s.n_nodes = n_nodes;
+  s.node_left = L.data(); s.node_right = R.data(); s.node_n = N.data(); s.node_index = I.data();
+  s.node_aa = aa.data(); s.node_bb = bb.data();
+  return rt_set_scene(c, &s);
+}
+
+int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_material* m) {
+  if (!c || !m || first < 0 || count < 0) return RT_ERR_ARG;
+  if (!c->scene_set) return fail(c, RT_ERR_STATE, "no scene");
+  if ((int64_t)first + count > c->n_tri) return fail(c, RT_ERR_ARG, "range outside the triangle list");
+  HIPCHK(c, hipSetDevice(c->device));
+  float packed[32];
+  pack_material(*m, packed);
+  int id = -1;
+  for (int k = 0; k < c->n_mats; k++)
+    if (!memcmp(&c->mat_table[32 * k], packed, sizeof(packed))) { id = k; break; }
+  if (id < 0) {
+    id = c->n_mats;
+    c->mat_table.resize(32 * (size_t)(id + 1));
+    memcpy(&c->mat_table[32 * id], packed, sizeof(packed));
+    c->n_mats++;
+    int rc = upload(c, (void**)&c->d_mats, c->mat_table.data(), c->mat_table.size() * sizeof(float));
+    if (rc) return rc;
+  }
+  for (int i = first; i < first + count; i++) {
+    c->tri_mat[i] = id;
+    // only the .w of the first normal texel carries the id: patch it in place
+    HIPCHK(c, hipMemcpyAsync(reinterpret_cast<char*>(c->d_trin + 3 * (size_t)i) + 12, &id, 4, hipMemcpyHostToDevice,
+                             c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32_t h, int32_t res) {
+  if (!c || !hdr || !cache || w <= 0 || h <= 0) return RT_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<float4> a((size_t)w * h), b((size_t)w * h);
+  for (size_t i = 0; i < a.size(); i++) {
+    a[i] = make_float4(hdr[3 * i], hdr[3 * i + 1], hdr[3 * i + 2], 0.0f);
+    b[i] = make_float4(cache[3 * i], cache[3 * i + 1], cache[3 * i + 2], 0.0f);
+  }
+  int rc;
+  if ((rc = upload(c, (void**)&c->d_hdr, a.data(), a.size() * sizeof(float4)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_cache, b.data(), b.size() * sizeof(float4)))) return rc;
+  c->hdr_w = w; c->hdr_h = h; c->hdr_res = res;
+  c->env_set = true;
+  return RT_OK;
+}
+
+int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
+  if (!c || width <= 0 || height <= 0) return RT_ERR_ARG;
+  rt_tiling tl = t ? *t : rt_tiling{32, 32, 0, 1};
+  if (tl.tile_w <= 0 || tl.tile_h <= 0 || (tl.tile_w % 8) || (tl.tile_h % 8) || tl.world <= 0 || tl.rank < 0 ||
+      tl.rank >= tl.world)
+    return fail(c, RT_ERR_ARG, "bad tiling (tile sizes must be positive multiples of 8, 0 <= rank < world)");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->W = width; c->H = height;
+  c->tile_w = tl.tile_w; c->tile_h = tl.tile_h; c->rank = tl.rank; c->world = tl.world;
+  c->tiles_x = (width + tl.tile_w - 1) / tl.tile_w;
+  c->tiles_y = (height + tl.tile_h - 1) / tl.tile_h;
+  int total = c->tiles_x * c->tiles_y;
+  c->local_tiles = total > tl.rank ? (total - tl.rank + tl.world - 1) / tl.world : 0;
+  c->max_local_tiles = (total + tl.world - 1) / tl.world;
+  dfree(c->d_accum);
+  size_t bytes = (size_t)std::max(1, c->max_local_tiles) * tl.tile_w * tl.tile_h * sizeof(float4);
+  HIPCHK(c, hipMalloc(&c->d_accum, bytes));
+  HIPCHK(c, hipMemset(c->d_accum, 0, bytes));
+  c->frame_set = true;
+  c->loop_num = 0;
+  return RT_OK;
+}
+
+int rt_reset(rt_ctx* c) {
+  if (!c) return RT_ERR_ARG;
+  c->loop_num = 0;
+  return RT_OK;
+}
+int rt_set_loop_num(rt_ctx* c, int32_t n) {
+  if (!c || n < 0) return RT_ERR_ARG;
+  c->loop_num = n;
+  return RT_OK;
+}
+int rt_get_loop_num(const rt_ctx* c, int32_t* n) {
+  if (!c || !n) return RT_ERR_ARG;
+  *n = c->loop_num;
+  return RT_OK;
+}
+int rt_clear_accum(rt_ctx* c) {
+  if (!c) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  HIPCHK(c, hipSetDevice(c->device));
+  size_t bytes = (size_t)std::max(1, c->max_local_tiles) * c->tile_w * c->tile_h * sizeof(float4);
+  HIPCHK(c, hipMemsetAsync(c->d_accum, 0, bytes, c->stream));
+  return RT_OK;
+}
+
+int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames) {
+  if (!c || !fp || n_frames < 0 || (n_frames && !rand_origin)) return RT_ERR_ARG;
+  if (!c->scene_set || !c->env_set || !c->frame_set) return fail(c, RT_ERR_STATE, "set_scene, set_env and resize first");
+  HIPCHK(c, hipSetDevice(c->device));
+  int done = 0;
+  while (done < n_frames) {
+    KParams P;
+    memset(&P, 0, sizeof(P));
+    int nf = 0;
+    // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12)
+    while (done < n_frames && nf < RT_MAX_FRAMES_PER_LAUNCH) {
+      if (fp->max_iterations == -1 || c->loop_num < fp->max_iterations) c->loop_num++;
+      bool traced = fp->max_iterations == -1 || c->loop_num < fp->max_iterations;
+      done++;
+      if (!traced) continue;
+      P.loop_num[nf] = c->loop_num;
+      P.rand_origin[nf] = rand_origin[done - 1];
+      nf++;
+    }
+    if (nf == 0) continue;
+    memcpy(P.pos, fp->position, 12); memcpy(P.lbc, fp->left_bottom_corner, 12);
+    memcpy(P.right, fp->right, 12); memcpy(P.up, fp->up, 12);
+    P.half_w = fp->half_w; P.half_h = fp->half_h;
+    P.enable_mis = fp->enable_mis; P.enable_env = fp->enable_env_map; P.enable_bsdf = fp->enable_bsdf;
+    P.env_intensity = fp->env_intensity; P.env_angle = fp->env_angle;
+    P.max_bounce = fp->max_bounce; P.flags = fp->flags; P.n_frames = nf;
+    P.W = c->W; P.H = c->H; P.tile_w = c->tile_w; P.tile_h = c->tile_h; P.tiles_x = c->tiles_x;
+    P.rank = c->rank; P.world = c->world;
+    P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
+    P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
+    P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
+    P.hdr = c->d_hdr; P.cache = c->d_cache; P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
+    P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
+    if (P.n_work == 0) continue;
+    HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 4, c->stream));
+    unsigned int max_blocks = (P.n_work + 255) / 256;
+    unsigned int grid = std::min<unsigned int>((unsigned)(c->n_cus * c->blocks_per_cu), max_blocks);
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    if (fp->flags & RT_FLAG_COUNT_VISITS)
+      hipLaunchKernelGGL(rtd::rt_path_kernel<true>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
+    else
+      hipLaunchKernelGGL(rtd::rt_path_kernel<false>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    c->events.push_back({e0, e1});
+    c->launches++;
+  }
+  return RT_OK;
+}
+
+int rt_synchronize(rt_ctx* c) {
+  if (!c) return RT_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (auto& e : c->events) {
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
+    c->kernel_ms += ms;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  c->events.clear();
+  return RT_OK;
+}
+
+int rt_stats_get(rt_ctx* c, rt_stats* st) {
+  if (!c || !st) return RT_ERR_ARG;
+  int rc = rt_synchronize(c);
+  if (rc) return rc;
+  unsigned long long h[8];
+  HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  st->rays = h[0]; st->samples = h[1]; st->internal_pops = h[2]; st->leaf_pops = h[3]; st->tri_tests = h[4];
+  st->launches = c->launches;
+  st->kernel_ms = c->kernel_ms;
+  return RT_OK;
+}
+
+int rt_stats_reset(rt_ctx* c) {
+  if (!c) return RT_ERR_ARG;
+  int rc = rt_synchronize(c);
+  if (rc) return rc;
+  HIPCHK(c, hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+  c->kernel_ms = 0.0;
+  c->launches = 0;
+  return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, rt_stats* st) {
+  int rc = rt_render_async(c, fp, rand_origin, n_frames);
+  if (rc) return rc;
+  return st ? rt_stats_get(c, st) : rt_synchronize(c);
+}
+
+int rt_get_stream(const rt_ctx* c, void** stream) {
+  if (!c || !stream) return RT_ERR_ARG;
+  *stream = (void*)c->stream;
+  return RT_OK;
+}
+
+int rt_set_stream(rt_ctx* c, void* stream) {
+  if (!c) return RT_ERR_ARG;
+  int rc = rt_synchronize(c);
+  if (rc) return rc;
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+    c->own_stream = false;
+  } else {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return RT_OK;
+}
+
+static int accum_transfer(rt_ctx* c, float* host, int32_t layout, bool to_host) {
+  if (!c || !host || (layout != RT_LAYOUT_FRAME && layout != RT_LAYOUT_LOCAL_TILES)) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  int rc = rt_synchronize(c);
+  if (rc) return rc;
+  const size_t tpx = (size_t)c->tile_w * c->tile_h;
+  std::vector<float4> buf((size_t)std::max(1, c->max_local_tiles) * tpx);
+  HIPCHK(c, hipMemcpy(buf.data(), c->d_accum, buf.size() * sizeof(float4), hipMemcpyDeviceToHost));
+  for (int lt = 0; lt < c->local_tiles; lt++) {
+    int gt = c->rank + lt * c->world;
+    int tx = gt % c->tiles_x, ty = gt / c->tiles_x;
+    for (int ly = 0; ly < c->tile_h; ly++)
+      for (int lx = 0; lx < c->tile_w; lx++) {
+        size_t li = (size_t)lt * tpx + (size_t)ly * c->tile_w + lx;
+        float* h;
+        if (layout == RT_LAYOUT_LOCAL_TILES) {
+          h = host + 3 * li;
+        } else {
+          int px = tx * c->tile_w + lx, py = ty * c->tile_h + ly;
+          if (px >= c->W || py >= c->H) continue;
+          h = host + 3 * ((size_t)py * c->W + px);
+        }
+        if (to_host) { h[0] = buf[li].x; h[1] = buf[li].y; h[2] = buf[li].z; }
+        else buf[li] = make_float4(h[0], h[1], h[2], 0.0f);
+      }
+  }
+  if (!to_host) HIPCHK(c, hipMemcpy(c->d_accum, buf.data(), buf.size() * sizeof(float4), hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+int rt_read_accum(rt_ctx* c, float* rgb_out, int32_t layout) { return accum_transfer(c, rgb_out, layout, true); }
+int rt_write_accum(rt_ctx* c, const float* rgb_in, int32_t layout) {
+  return accum_transfer(c, const_cast<float*>(rgb_in), layout, false);
+}
+
+int rt_accum_device(const rt_ctx* c, void** ptr, size_t* bytes, int32_t* local_tiles, int32_t* max_local_tiles) {
+  if (!c || !ptr || !bytes) return RT_ERR_ARG;
+  if (!c->frame_set) return RT_ERR_STATE;
+  *ptr = c->d_accum;
+  *bytes = (size_t)std::max(1, c->max_local_tiles) * c->tile_w * c->tile_h * sizeof(float4);
+  if (local_tiles) *local_tiles = c->local_tiles;
+  if (max_local_tiles) *max_local_tiles = c->max_local_tiles;
+  return RT_OK;
+}
+
+int rt_assemble_frame(rt_ctx* c, const void* gathered, int32_t world, void* frame) {
+  if (!c || !gathered || !frame || world <= 0) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  if (world != c->world) return fail(c, RT_ERR_ARG, "world differs from the tiling");
+  HIPCHK(c, hipSetDevice(c->device));
+  dim3 block(256), grid((c->W + 255) / 256, c->H);
+  hipLaunchKernelGGL(rtd::rt_assemble_kernel, grid, block, 0, c->stream, (const float4*)gathered, (float*)frame, c->W,
+                     c->H, c->tile_w, c->tile_h, c->tiles_x, world, std::max(1, c->max_local_tiles));
+  HIPCHK(c, hipGetLastError());
+  return RT_OK;
+}
+
+}  // extern "C"
