@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/sec + ms/frame of the MI355X path tracer (BASELINE.json metric).
+
+Workload (default): config C3 = floor + loong_100000 (copper), 1920x1080, maxBounce 8,
+HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs.py).
+One *step* = ``--frames-per-step`` progressive frames (1 spp each) of the whole frame,
+rendered by one kernel launch per rank over that rank's pixel tiles, followed by the
+frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
+torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
+
+    python bench.py [--gpus 1] [--steps 10] [--warmup 2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  value = rays traced by all ranks / max-over-ranks wall time
+of the timed steps (barrier + synchronize on both sides).  Rays are counted on the device
+(camera + NEE shadow + continuation = every hitBVH call of the reference, RT:1386/1480/1528).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "opengl-ray-tracing-framework_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# algorithmic bytes per traversal from the reference's visit counts
+#   64 B per internal pop (16 B node ints + two 24-B child AABBs), 16 B per leaf pop,
+#   36 B per triangle test (positions), 132 B per closer-hit update (normals + material),
+#   12 B per HDR texel fetch, 12 B per cache texel fetch, + 24 B per pixel-frame (accum r/w)
+B_INT, B_LEAF, B_TRI, B_UPD, B_ENV, B_CACHE, B_PIXEL = 64, 16, 36, 132, 12, 12, 24
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--frames-per-step", type=int, default=4)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-baseline sample: oracle frames until this wall time (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
+    return ap.parse_args()
+
+
+def cpu_baseline(sd, env, W, H, fp, seconds: float, threads: int):
+    """The oracle (CPU restatement of the shader, OpenMP) on whole frames 1..k of the same
+    workload until `seconds` of wall time; returns the JSON object and the §8(d) counters."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as orc  # cpu_baseline leg only: the checker, timed as the reference-algorithm baseline
+    from rtamd import configs as cf
+
+    if threads <= 0:
+        try:
+            threads = min(16, len(os.sched_getaffinity(0)))
+        except AttributeError:
+            threads = min(16, os.cpu_count() or 1)
+    scene = orc.OracleScene(sd.tri_enc, sd.node_enc, env[0], env[1])
+    ro = cf.rand_origins(32)
+    acc = None
+    tot = None
+    t0 = time.perf_counter()
+    k = 0
+    while k < 32:
+        acc, cnt = orc.render(scene, [cf.oracle_frame_params(fp, k + 1, ro[k])], W, H, accum=acc, threads=threads)
+        tot = cnt if tot is None else {key: tot[key] + cnt[key] for key in tot}
+        k += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    obj = {"value": round(tot["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/rt_oracle.cpp (CPU restatement of the GLSL path, no culling) on {k} full "
+                     f"{W}x{H} frame(s) of the same workload, {tot['rays']} rays in {dt:.1f} s; "
+                     "llvmpipe GL baseline unavailable (no GL/EGL context, SURVEY §8(c))",
+           "ms_per_frame": round(dt * 1e3 / k, 1)}
+    return obj, tot
+
+
+def main() -> int:
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus N>1 must be launched with torch.distributed.run (one process per GPU)",
+                  file=sys.stderr)
+            return 2
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(local_rank)
+
+    from rtamd import configs as cf
+    from rtamd.renderer import RT_FLAG_COUNT_VISITS, Renderer
+
+    cfg = cf.CONFIGS[args.config]
+    W, H = args.width or cfg.width, args.height or cfg.height
+    F, steps, warm = args.frames_per_step, args.steps, args.warmup
+    total_frames = (warm + steps) * F + 1
+    sd = cf.config_scene(args.config)
+    env = cf.load_env()
+    fp = cf.frame_params(W, H)
+
+    r = Renderer(local_rank)
+    stream = torch.cuda.current_stream()
+    r.set_stream(stream.cuda_stream)  # kernels, copies and RCCL collectives on one stream
+    r.set_scene_soa(sd.soa, sd.nodes)
+    r.set_env(*env)
+    r.resize(W, H, tile=args.tile, rank=rank, world=world)
+    info = r.device_info()
+    ad = r.accum_device()
+    nfloat = ad["bytes"] // 4
+    local = torch.empty(nfloat, dtype=torch.float32, device="cuda")
+    gathered = torch.empty(world * nfloat, dtype=torch.float32, device="cuda") if rank == 0 else None
+    frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
+    ro = cf.rand_origins(total_frames)
+
+    def step(k: int) -> None:
+        r.render_async(fp, ro[k * F:(k + 1) * F])
+        if args.no_gather:
+            return
+        if world == 1:
+            r.assemble_frame(ad["ptr"], 1, frame.data_ptr())
+            return
+        r.copy_accum_device(local.data_ptr(), ad["bytes"])
+        parts = list(gathered.view(world, nfloat).unbind(0)) if rank == 0 else None
+        dist.gather(local, gather_list=parts, dst=0)
+        if rank == 0:
+            r.assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
+
+    for k in range(warm):
+        step(k)
+    torch.cuda.synchronize()
+    r.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(warm, warm + steps):
+        step(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+
+    # whole-job aggregates
+    vals = torch.tensor([elapsed, float(st["rays"]), float(st["samples"])], dtype=torch.float64, device="cuda")
+    if dist:
+        t_max = vals[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        sums = vals[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed, rays, samples = float(t_max[0]), float(sums[0]), float(sums[1])
+    else:
+        rays, samples = float(st["rays"]), float(st["samples"])
+
+    # own-traversal visit counts (one extra frame, outside the timed region)
+    r.reset_stats()
+    r.render(cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS), ro[-1:])
+    vis = r.stats()
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
+
+    launch_ms = st["kernel_ms"] / max(1, st["launches"])
+    out = {
+        "metric": METRIC,
+        "value": round(rays / elapsed / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": round(elapsed * 1e3 / steps, 3),
+        "ms_per_frame": round(elapsed * 1e3 / (steps * F), 3),
+        "msamples_per_s": round(samples / elapsed / 1e6, 2),
+        "rays_per_sample": round(rays / max(1.0, samples), 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "reference scene assets (loong_100000.obj, floor.obj, peppermint_powerplant_1k.hdr); "
+                "randOrigin from glibc srand(20221002)",
+        "config": {"workload": f"{cfg.name}: {cfg.note}; {W}x{H}, maxBounce 8, BSDF+MIS+env",
+                   "width": W, "height": H, "frames_per_step": F, "spp_timed": steps * F,
+                   "tile": args.tile, "parallelism": f"pixel-tiles x{world} + frame-end gather",
+                   "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
+        "kernel": {"name": "rt_path_kernel", "avg_launch_ms": round(launch_ms, 4), "launches": st["launches"],
+                   "grid_blocks_per_cu": info["blocks_per_cu"], "lds_bytes_per_block": info["lds_bytes_per_block"]},
+        "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
+    }
+    if vis["rays"]:
+        out["own_traversal_per_ray"] = {"internal": round(vis["internal_pops"] / vis["rays"], 2),
+                                        "leaf": round(vis["leaf_pops"] / vis["rays"], 2),
+                                        "tri": round(vis["tri_tests"] / vis["rays"], 2)}
+
+    # CPU baseline (rank 0, N = 1 only) and the §8(d) per-ray byte figure from its counters
+    cnt = None
+    if world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"], cnt = cpu_baseline(sd, env, W, H, fp, args.cpu_seconds, args.cpu_threads)
+    pmc = ROOT / "profiles" / f"pmc_traffic_{args.config}.json"
+    traffic = None
+    if pmc.exists():
+        p = json.loads(pmc.read_text())
+        if p.get("width") == W and p.get("height") == H and p.get("frames_per_launch") == F:
+            traffic = p.get("hbm_bytes_per_launch")
+    if cnt is not None:
+        per_sample = (B_INT * cnt["internal_pops"] + B_LEAF * cnt["leaf_pops"] + B_TRI * cnt["tri_tests"] +
+                      B_UPD * cnt["closer_updates"] + B_ENV * cnt["env_fetches"] +
+                      B_CACHE * cnt["cache_fetches"]) / cnt["samples"] + B_PIXEL
+        samples_per_launch = st["samples"] / max(1, st["launches"])
+        bytes_per_launch = per_sample * samples_per_launch
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                           "algorithmic_bytes_per_sample": round(per_sample, 1),
+                           "bytes_per_launch": round(bytes_per_launch),
+                           "note": "algorithmic bytes from the reference traversal's visit counts (SURVEY §8(d)); "
+                                   "working set fits the 256 MiB Infinity Cache, so HBM is not the limiter"}
+    else:
+        out["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                           "traffic": traffic, "note": "per-ray bytes need the rank-0 N=1 oracle sample"}
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

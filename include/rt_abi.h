@@ -149,6 +149,9 @@ int rt_write_accum(rt_ctx* ctx, const float* rgb_in, int32_t layout);
  * max_local_tiles tiles so that every rank's buffer has the same size. */
 int rt_accum_device(const rt_ctx* ctx, void** device_ptr, size_t* bytes, int32_t* local_tiles,
                     int32_t* max_local_tiles);
+/* Device-to-device copy of the accumulation buffer (rt_accum_device bytes) into dst, enqueued
+ * on the ctx stream (feeds the frame-end gather). */
+int rt_copy_accum_device(rt_ctx* ctx, void* dst_device, size_t bytes);
 /* Un-permute `world` gathered accumulation buffers (rank-major, each rt_accum_device bytes) on
  * this ctx's device into a width*height*3 float frame (device pointer). */
 int rt_assemble_frame(rt_ctx* ctx, const void* gathered_device, int32_t world, void* frame_device);

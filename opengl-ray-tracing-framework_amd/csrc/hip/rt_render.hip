@@ -562,6 +562,16 @@ int rt_accum_device(const rt_ctx* c, void** ptr, size_t* bytes, int32_t* local_t
   return RT_OK;
 }
 
+int rt_copy_accum_device(rt_ctx* c, void* dst, size_t bytes) {
+  if (!c || !dst) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  size_t have = (size_t)std::max(1, c->max_local_tiles) * c->tile_w * c->tile_h * sizeof(float4);
+  if (bytes > have) return fail(c, RT_ERR_ARG, "copy larger than the accumulation buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(dst, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return RT_OK;
+}
+
 int rt_assemble_frame(rt_ctx* c, const void* gathered, int32_t world, void* frame) {
   if (!c || !gathered || !frame || world <= 0) return RT_ERR_ARG;
   if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");

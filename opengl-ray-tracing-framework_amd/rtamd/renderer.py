@@ -30,7 +30,8 @@ ABI_SYMBOLS = (
     "rt_create", "rt_destroy", "rt_last_error", "rt_device_info", "rt_set_scene", "rt_set_scene_encoded",
     "rt_update_materials", "rt_set_env", "rt_resize", "rt_reset", "rt_set_loop_num", "rt_get_loop_num",
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
-    "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_assemble_frame",
+    "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
+    "rt_assemble_frame",
 )
 
 
@@ -141,6 +142,7 @@ def lib() -> C.CDLL:
         L.rt_read_accum.argtypes = [vp, _f32p, C.c_int32]
         L.rt_write_accum.argtypes = [vp, _f32p, C.c_int32]
         L.rt_accum_device.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), _i32p, _i32p]
+        L.rt_copy_accum_device.argtypes = [vp, vp, C.c_size_t]
         L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
         _lib = L
     return _lib
@@ -305,6 +307,9 @@ class Renderer:
         self._check(self._L.rt_accum_device(self._h, C.byref(p), C.byref(n), C.byref(lt), C.byref(mlt)),
                     "rt_accum_device")
         return {"ptr": p.value, "bytes": n.value, "local_tiles": lt.value, "max_local_tiles": mlt.value}
+
+    def copy_accum_device(self, dst_ptr: int, nbytes: int) -> None:
+        self._check(self._L.rt_copy_accum_device(self._h, C.c_void_p(dst_ptr), nbytes), "rt_copy_accum_device")
 
     def assemble_frame(self, gathered_ptr: int, world: int, frame_ptr: int) -> None:
         self._check(self._L.rt_assemble_frame(self._h, C.c_void_p(gathered_ptr), world, C.c_void_p(frame_ptr)),

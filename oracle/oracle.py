@@ -35,7 +35,8 @@ class OrcFrame(C.Structure):
 
 class OrcCounters(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("internal_pops", C.c_uint64), ("leaf_pops", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("closer_updates", C.c_uint64), ("samples", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("closer_updates", C.c_uint64), ("samples", C.c_uint64),
+                ("env_fetches", C.c_uint64), ("cache_fetches", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

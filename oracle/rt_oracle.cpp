@@ -104,7 +104,7 @@ typedef struct {  // the per-frame uniforms of src/sources/main.cpp:181-199
 } orc_frame;
 
 typedef struct {  // traversal counters for SURVEY.md §8(d)
-  uint64_t rays, internal_pops, leaf_pops, tri_tests, closer_updates, samples;
+  uint64_t rays, internal_pops, leaf_pops, tri_tests, closer_updates, samples, env_fetches, cache_fetches;
 } orc_counters;
 }
 
@@ -434,7 +434,8 @@ vec2 toSphericalCoord(const Ctx& C, vec3 v) {  // RT:625-631 (R13: envAngle not 
   return vec2{uv.x + C.f->env_angle, uv.y + 0.0f};
 }
 
-vec3 SampleHdr(const Ctx& C, float xi_1, float xi_2) {  // RT:635-646 (R13: s = xi_1)
+vec3 SampleHdr(Ctx& C, float xi_1, float xi_2) {  // RT:635-646 (R13: s = xi_1)
+  C.c.cache_fetches++;
   vec3 c = tex2D(C.s->hdr_cache, C.s->hdr_w, C.s->hdr_h, vec2{xi_1, xi_2});
   vec2 xy = vec2{c.x, c.y};
   xy.y = 1.0f - xy.y;
@@ -644,12 +645,14 @@ vec3 DisneySample(float xi_1, float xi_2, float xi_3, const Material& material, 
   return f * fabs_(dot(N, L));
 }
 
-vec3 hdrColor(const Ctx& C, vec3 L) {  // RT:1165-1169
+vec3 hdrColor(Ctx& C, vec3 L) {  // RT:1165-1169
+  C.c.env_fetches++;
   vec2 uv = toSphericalCoord(C, normalize(L));
   return tex2D(C.s->hdr_map, C.s->hdr_w, C.s->hdr_h, uv);
 }
 
-float hdrPdf(const Ctx& C, vec3 L, int hdrResolution) {  // RT:1173-1186
+float hdrPdf(Ctx& C, vec3 L, int hdrResolution) {  // RT:1173-1186
+  C.c.cache_fetches++;
   vec2 uv = toSphericalCoord(C, normalize(L));
   float pdf = tex2D(C.s->hdr_cache, C.s->hdr_w, C.s->hdr_h, uv).z;
   float theta = PI * uv.y;
@@ -1030,6 +1033,7 @@ int orc_render(const orc_scene* scene, const orc_frame* frames, int n_frames, in
         local.rays += C.c.rays; local.internal_pops += C.c.internal_pops;
         local.leaf_pops += C.c.leaf_pops; local.tri_tests += C.c.tri_tests;
         local.closer_updates += C.c.closer_updates; local.samples += C.c.samples;
+        local.env_fetches += C.c.env_fetches; local.cache_fetches += C.c.cache_fetches;
       }
       a[0] = hist.x; a[1] = hist.y; a[2] = hist.z;
     }
@@ -1038,6 +1042,7 @@ int orc_render(const orc_scene* scene, const orc_frame* frames, int n_frames, in
       total.rays += local.rays; total.internal_pops += local.internal_pops;
       total.leaf_pops += local.leaf_pops; total.tri_tests += local.tri_tests;
       total.closer_updates += local.closer_updates; total.samples += local.samples;
+      total.env_fetches += local.env_fetches; total.cache_fetches += local.cache_fetches;
     }
   }
   if (counters) *counters = total;
@@ -1090,12 +1095,12 @@ float orc_dielectric_fresnel(float cos_i, float eta) { return DielectricFresnel(
 float orc_gtr2(float ndoth, float alpha) { return GTR2(ndoth, alpha); }
 float orc_hdr_pdf(const orc_scene* scene, const float* L, float env_angle) {
   orc_frame f; memset(&f, 0, sizeof(f)); f.env_angle = env_angle;
-  Ctx C; C.s = scene; C.f = &f;
+  Ctx C; C.s = scene; C.f = &f; memset(&C.c, 0, sizeof(C.c));
   return hdrPdf(C, vec3(L[0], L[1], L[2]), scene->hdr_resolution);
 }
 void orc_sample_hdr(const orc_scene* scene, float xi1, float xi2, float* L) {
   orc_frame f; memset(&f, 0, sizeof(f));
-  Ctx C; C.s = scene; C.f = &f;
+  Ctx C; C.s = scene; C.f = &f; memset(&C.c, 0, sizeof(C.c));
   vec3 v = SampleHdr(C, xi1, xi2);
   L[0] = v.x; L[1] = v.y; L[2] = v.z;
 }

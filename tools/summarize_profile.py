@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_gpu.sh output directory into profiles/<tag>_*.{csv,json}.
+
+traffic (HBM bytes per launch) = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, FETCH_SIZE doubled per
+MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B read requests at 64 B); that correction is
+calibrated for wide coalesced streams, this kernel's reads are 16-B-per-lane gathers, so the
+absolute value is indicative and the raw counters are kept beside it.
+"""
+import csv
+import json
+import shutil
+import statistics
+import sys
+from pathlib import Path
+
+src = Path(sys.argv[1])
+tag = sys.argv[2]
+cfg = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}
+dst = Path(__file__).resolve().parent.parent / "profiles"
+dst.mkdir(exist_ok=True)
+KERNEL = "rt_path_kernel<false>"
+
+shutil.copyfile(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
+durs = []
+for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")):
+    if KERNEL in r["Kernel_Name"]:
+        durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        vgpr, lds = r["VGPR_Count"], r["LDS_Block_Size"]
+
+
+def counters(name):
+    out = {}
+    for r in csv.DictReader(open(src / name / "run_counter_collection.csv")):
+        if KERNEL in r["Kernel_Name"]:
+            out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: statistics.mean(v) for k, v in out.items()}
+
+
+pf, pw, sq = counters("pmc_fetch"), counters("pmc_write"), counters("pmc_sq")
+summary = {
+    "kernel": KERNEL,
+    "launches_traced": len(durs),
+    "avg_launch_ms": round(statistics.mean(durs), 4),
+    "min_launch_ms": round(min(durs), 4),
+    "vgpr_count": int(vgpr), "lds_block_size": int(lds),
+    "FETCH_SIZE_kB_per_launch": round(pf["FETCH_SIZE"], 1),
+    "WRITE_SIZE_kB_per_launch": round(pw["WRITE_SIZE"], 1),
+    "hbm_bytes_per_launch": round((2 * pf["FETCH_SIZE"] + pw["WRITE_SIZE"]) * 1024),
+    "SQ": {k: v for k, v in sq.items()},
+    "valu_insts_per_wave": round(sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]),
+}
+summary.update(cfg)
+(dst / f"{tag}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
+print(json.dumps(summary, indent=1))
