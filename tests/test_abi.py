@@ -1,0 +1,41 @@
+"""The C-ABI libraries load and export every symbol their headers declare (no GPU calls)."""
+import ctypes as C
+import re
+
+import pytest
+
+from conftest import ROOT
+from rtamd import renderer, scene_lib
+
+
+def _declared(header):
+    text = (ROOT / "include" / header).read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(rt[s]?_\w+)\s*\(", text, re.M)))
+
+
+@pytest.mark.parametrize("header,libname", [("rt_abi.h", "librtamd.so"), ("rt_scene.h", "librtscene.so")])
+def test_library_exports_every_declared_symbol(header, libname):
+    syms = _declared(header)
+    assert len(syms) > 10
+    lib = C.CDLL(str(ROOT / "opengl-ray-tracing-framework_amd" / "lib" / libname))
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_abi():
+    assert sorted(renderer.ABI_SYMBOLS) == _declared("rt_abi.h")
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(RuntimeError, match="no usable HIP device"):
+        renderer.Renderer(0)
+
+
+def test_scene_lib_error_codes():
+    with pytest.raises(RuntimeError):
+        scene_lib.Mesh.load("/nonexistent.obj")
+    with pytest.raises(RuntimeError):
+        scene_lib.load_hdr("/nonexistent.hdr")
