@@ -92,15 +92,21 @@ typedef struct rt_frame_params {
 
 enum {
   RT_FLAG_NO_CULL = 1,            /* disable closest-hit box culling (exhaustive RT:338 order)  */
-  RT_FLAG_COUNT_VISITS = 2        /* also count node/triangle visits (slower)                  */
+  RT_FLAG_COUNT_VISITS = 2,       /* also count node/triangle visits (slower)                  */
+  RT_FLAG_MEGAKERNEL = 4,         /* single persistent megakernel instead of the wavefront path */
+  RT_FLAG_TRACE_WHOLE = 8         /* wavefront traversal: whole ray per lane between refills    */
 };
 
 typedef struct rt_stats {
   uint64_t rays;            /* hitBVH invocations: camera + NEE shadow + continuation    */
   uint64_t samples;         /* pixel samples traced (frames x pixels, R12 copies excluded) */
   uint64_t internal_pops, leaf_pops, tri_tests;  /* only with RT_FLAG_COUNT_VISITS */
-  uint64_t launches;
-  double kernel_ms;         /* sum of kernel durations (HIP events) since rt_stats_reset  */
+  uint64_t launches;        /* rt_render_async calls that launched work                  */
+  double kernel_ms;         /* GPU time of those calls (HIP events on the ctx stream)     */
+  uint64_t trace_launches;  /* traversal kernel launches (wavefront) / megakernel launches */
+  double trace_ms;          /* summed duration of those launches (HIP events around each) */
+  uint64_t trace_iters;     /* RT_FLAG_COUNT_VISITS: traversal loop iterations, all waves */
+  uint64_t trace_iters_max; /* RT_FLAG_COUNT_VISITS: max loop iterations of one wave       */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

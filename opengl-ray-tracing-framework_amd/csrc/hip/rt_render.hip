@@ -5,6 +5,7 @@
 // entry point returns RT_ERR_NODEVICE / RT_ERR_HIP.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -14,6 +15,7 @@
 
 #include "rt_abi.h"
 #include "rt_kernels.h"
+#include "rt_wavefront.h"
 
 using rtd::GNode;
 using rtd::KParams;
@@ -47,10 +49,20 @@ struct rt_ctx {
   // counters
   unsigned int* d_counter = nullptr;
   unsigned long long* d_stats = nullptr;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
-  double kernel_ms = 0.0;
-  uint64_t launches = 0;
-  int blocks_per_cu = 0, block_lds = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;        // whole render calls
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> trace_events;  // traversal launches
+  std::vector<hipEvent_t> event_pool;
+  double kernel_ms = 0.0, trace_ms = 0.0;
+  uint64_t launches = 0, trace_launches = 0;
+  int blocks_per_cu = 0, block_lds = 0;      // megakernel
+  int trace_bpc = 0;                          // wavefront traversal kernel
+  // wavefront path state (one slot per local pixel)
+  void* wf_mem = nullptr;
+  size_t wf_paths = 0;
+  rtd::WFState wf{};
+  unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
+  int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
+  int frames_cap = 1;              // frames in flight per wavefront
 };
 
 namespace {
@@ -105,9 +117,44 @@ int occupancy(rt_ctx* c) {
   int lds = c->stack_entries * 256 * 8;
   int bpc = 0;
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::rt_path_kernel<false>, 256, lds));
-  if (bpc < 1) bpc = 1;
-  c->blocks_per_cu = bpc;
+  c->blocks_per_cu = std::max(1, bpc);
   c->block_lds = lds;
+  bpc = 0;
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false>, 256, lds));
+  c->trace_bpc = std::max(1, bpc);
+  return RT_OK;
+}
+
+hipEvent_t take_event(rt_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Path-state buffers of the wavefront path, carved from one allocation.
+int alloc_wavefront(rt_ctx* c, size_t paths) {
+  if (c->wf_mem && c->wf_paths >= paths) return RT_OK;
+  if (c->wf_mem) { (void)hipFree(c->wf_mem); c->wf_mem = nullptr; }
+  const size_t P = std::max<size_t>(paths, 64);
+  const size_t bytes = P * (6 * 16 + 4 * 16 + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
+  HIPCHK(c, hipMalloc(&c->wf_mem, bytes));
+  char* p = static_cast<char*>(c->wf_mem);
+  auto carve = [&](size_t n) { char* q = p; p += (n + 255) & ~size_t(255); return q; };
+  c->wf.s0 = (float4*)carve(P * 16); c->wf.s1 = (float4*)carve(P * 16); c->wf.s2 = (float4*)carve(P * 16);
+  c->wf.s3 = (float4*)carve(P * 16); c->wf.s4 = (float4*)carve(P * 16); c->wf.s5 = (uint4*)carve(P * 16);
+  c->wf.ro = (float4*)carve(P * 16); c->wf.rd = (float4*)carve(P * 16);
+  c->wf.so = (float4*)carve(P * 16); c->wf.sd = (float4*)carve(P * 16);
+  c->wf.res = (int2*)carve(P * 16);
+  c->wf.fin = (float4*)carve(P * 16);
+  c->wf.queue[0] = (int*)carve(P * 8); c->wf.queue[1] = (int*)carve(P * 8);
+  c->wf.active[0] = (int*)carve(P * 4); c->wf.active[1] = (int*)carve(P * 4);
+  c->wf.cnt = (unsigned int*)carve(64);
+  c->wf_paths = P;
   return RT_OK;
 }
 
@@ -146,6 +193,10 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   dfree(c->d_nodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
   dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
+  for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->wf_mem) (void)hipFree(c->wf_mem);
+  dfree(c->d_pix);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -371,6 +422,37 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   size_t bytes = (size_t)std::max(1, c->max_local_tiles) * tl.tile_w * tl.tile_h * sizeof(float4);
   HIPCHK(c, hipMalloc(&c->d_accum, bytes));
   HIPCHK(c, hipMemset(c->d_accum, 0, bytes));
+  // pixel list of this rank: its tiles in order, 8x8 blocks inside a tile (ray coherence)
+  std::vector<unsigned int> xy, acc;
+  const int tpx = tl.tile_w * tl.tile_h;
+  for (int lt = 0; lt < c->local_tiles; lt++) {
+    const int gt = tl.rank + lt * tl.world;
+    const int tx = gt % c->tiles_x, ty = gt / c->tiles_x;
+    for (int r = 0; r < tpx; r++) {
+      const int blk = r >> 6, in = r & 63, bxs = tl.tile_w >> 3;
+      const int lx = (blk % bxs) * 8 + (in & 7), ly = (blk / bxs) * 8 + (in >> 3);
+      const int px = tx * tl.tile_w + lx, py = ty * tl.tile_h + ly;
+      if (px >= width || py >= height) continue;
+      xy.push_back((unsigned)px | ((unsigned)py << 16));
+      acc.push_back((unsigned)(lt * tpx + ly * tl.tile_w + lx));
+    }
+  }
+  if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
+  c->n_valid = (int)xy.size();
+  dfree(c->d_pix);
+  const size_t nv = std::max<size_t>(1, xy.size());
+  HIPCHK(c, hipMalloc(&c->d_pix, 2 * nv * sizeof(unsigned int)));
+  if (!xy.empty()) {
+    HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
+  }
+  size_t max_slots = 8u << 20;  // ~1.8 GB of path state
+  if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
+  c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / nv));
+  int rc = alloc_wavefront(c, (size_t)c->frames_cap * nv);
+  if (rc) return rc;
+  c->wf.pix_xy = c->d_pix;
+  c->wf.pix_acc = c->d_pix + nv;
   c->frame_set = true;
   c->loop_num = 0;
   return RT_OK;
@@ -410,7 +492,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     memset(&P, 0, sizeof(P));
     int nf = 0;
     // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12)
-    while (done < n_frames && nf < RT_MAX_FRAMES_PER_LAUNCH) {
+    const int cap = (fp->flags & RT_FLAG_MEGAKERNEL) ? RT_MAX_FRAMES_PER_LAUNCH : c->frames_cap;
+    while (done < n_frames && nf < cap) {
       if (fp->max_iterations == -1 || c->loop_num < fp->max_iterations) c->loop_num++;
       bool traced = fp->max_iterations == -1 || c->loop_num < fp->max_iterations;
       done++;
@@ -434,18 +517,60 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.hdr = c->d_hdr; P.cache = c->d_cache; P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
     if (P.n_work == 0) continue;
-    HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 4, c->stream));
-    unsigned int max_blocks = (P.n_work + 255) / 256;
-    unsigned int grid = std::min<unsigned int>((unsigned)(c->n_cus * c->blocks_per_cu), max_blocks);
-    hipEvent_t e0, e1;
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
+    const bool count = (fp->flags & RT_FLAG_COUNT_VISITS) != 0;
+    hipEvent_t e0 = take_event(c), e1 = take_event(c);
+    if (!e0 || !e1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
     HIPCHK(c, hipEventRecord(e0, c->stream));
-    if (fp->flags & RT_FLAG_COUNT_VISITS)
-      hipLaunchKernelGGL(rtd::rt_path_kernel<true>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
-    else
-      hipLaunchKernelGGL(rtd::rt_path_kernel<false>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
-    HIPCHK(c, hipGetLastError());
+    if (fp->flags & RT_FLAG_MEGAKERNEL) {
+      HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 4, c->stream));
+      unsigned int max_blocks = (P.n_work + 255) / 256;
+      unsigned int grid = std::min<unsigned int>((unsigned)(c->n_cus * c->blocks_per_cu), max_blocks);
+      if (count)
+        hipLaunchKernelGGL(rtd::rt_path_kernel<true>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
+      else
+        hipLaunchKernelGGL(rtd::rt_path_kernel<false>, dim3(grid), dim3(256), c->block_lds, c->stream, P);
+      HIPCHK(c, hipGetLastError());
+      c->trace_launches++;
+    } else {
+      rtd::WFParams WP;
+      WP.K = P;
+      WP.K.n_work = (unsigned)c->n_valid;
+      WP.S = c->wf;
+      WP.n_frames = nf;
+      const unsigned int slots = (unsigned)nf * (unsigned)c->n_valid;
+      const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots + 255) / 256));
+      const unsigned int shade_grid = gen_grid;
+      unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
+      if (const char* g = getenv("RT_TRACE_GRID")) trace_grid = (unsigned)atoi(g);  // experiments
+      const bool whole = (fp->flags & RT_FLAG_TRACE_WHOLE) != 0;
+      HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));
+      WP.pass = 0;
+      hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, c->stream, WP);
+      HIPCHK(c, hipGetLastError());
+      for (int pass = 0; pass <= std::max(0, fp->max_bounce); pass++) {
+        WP.pass = pass;
+        hipEvent_t t0 = take_event(c), t1 = take_event(c);
+        if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+        HIPCHK(c, hipEventRecord(t0, c->stream));
+        if (count && whole)
+          hipLaunchKernelGGL(rtd::wf_trace_whole<true>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+        else if (whole)
+          hipLaunchKernelGGL(rtd::wf_trace_whole<false>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+        else if (count)
+          hipLaunchKernelGGL(rtd::wf_trace<true>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+        else
+          hipLaunchKernelGGL(rtd::wf_trace<false>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(t1, c->stream));
+        c->trace_events.push_back({t0, t1});
+        c->trace_launches++;
+        hipLaunchKernelGGL(rtd::wf_shade, dim3(shade_grid), dim3(256), 0, c->stream, WP);
+        HIPCHK(c, hipGetLastError());
+      }
+      const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
+      hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, c->stream, WP);
+      HIPCHK(c, hipGetLastError());
+    }
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->events.push_back({e0, e1});
     c->launches++;
@@ -461,10 +586,18 @@ int rt_synchronize(rt_ctx* c) {
     float ms = 0.0f;
     HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
     c->kernel_ms += ms;
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
+    c->event_pool.push_back(e.first);
+    c->event_pool.push_back(e.second);
   }
   c->events.clear();
+  for (auto& e : c->trace_events) {
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
+    c->trace_ms += ms;
+    c->event_pool.push_back(e.first);
+    c->event_pool.push_back(e.second);
+  }
+  c->trace_events.clear();
   return RT_OK;
 }
 
@@ -477,6 +610,10 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->rays = h[0]; st->samples = h[1]; st->internal_pops = h[2]; st->leaf_pops = h[3]; st->tri_tests = h[4];
   st->launches = c->launches;
   st->kernel_ms = c->kernel_ms;
+  st->trace_launches = c->trace_launches;
+  st->trace_ms = c->trace_ms;
+  st->trace_iters = h[5];
+  st->trace_iters_max = h[6];
   return RT_OK;
 }
 
@@ -487,6 +624,8 @@ int rt_stats_reset(rt_ctx* c) {
   HIPCHK(c, hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
   c->kernel_ms = 0.0;
   c->launches = 0;
+  c->trace_ms = 0.0;
+  c->trace_launches = 0;
   return RT_OK;
 }
 

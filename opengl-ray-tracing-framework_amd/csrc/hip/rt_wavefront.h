@@ -1,0 +1,629 @@
+// rt_wavefront.h — wavefront formulation of the path tracer for gfx950.
+//
+// The reference runs one fragment per pixel that loops over bounces (RT:1369-1516).  On a
+// 64-wide wavefront that megakernel form mixes traversal with long, divergent shading code and
+// pins ~170 VGPRs for the whole path.  Here a frame is a sequence of small kernels over
+// device-resident path state (one slot per pixel of this rank):
+//
+//   wf_gen     camera ray per pixel (RT:1520-1527)                  -> ray queue, active list
+//   wf_trace   closest-hit / any-hit BVH traversal of every queued   -> (triangle, t) per ray
+//              ray, persistent grid with per-lane dynamic ray fetch
+//   wf_shade   per active path: apply the NEE result (RT:1389-1405),  -> next rays, next list
+//              the medium-emissive term (RT:1437-1439), the continuation result (RT:1483-1510),
+//              then the next bounce's light sample, DisneySample, media and DisneyEval
+//              (RT:1376-1474); finished paths blend into the accumulation (RT:1552)
+//
+// wf_trace + wf_shade repeat maxBounce+1 times; passes with no work exit at once.  All frames
+// of one launch are in flight together (path slot = frame * n_work + pixel): a pixel's frames
+// are independent until the progressive blend, so wf_blend applies RT:1552 afterwards in frame
+// order, exactly as sequential frames would.  This amortises the serial tail of the deepest
+// rays of each pass over several frames.  Shadow and continuation rays of all paths share one
+// traversal launch.  Every value that
+// reaches the image is computed with the same fp32 operations, in the same order, as the
+// oracle (the pending NEE term is added to Lo before the medium term and before the
+// continuation term, as in the shader), so results stay bit-identical.
+#pragma once
+#include "rt_kernels.h"
+
+namespace rtd {
+
+// per-path flags
+enum : uint32_t {
+  PF_SHADOW = 1u,      // a shadow ray was traced for the current bounce (c_nee pending)
+  PF_CMED = 2u,        // medium-emissive term pending (RT:1438)
+  PF_CONT = 4u,        // a continuation ray is queued (else the path ends after the shadow ray)
+  PF_MEDIUM = 8u,      // mediumSampled (RT:1444)
+  PF_CAMERA = 16u      // the queued continuation ray is the camera ray
+};
+
+struct WFState {
+  float4* __restrict__ s0;   // hist.xyz, evp
+  float4* __restrict__ s1;   // Lo.xyz, Le0.x
+  float4* __restrict__ s2;   // evf.xyz, Le0.y
+  float4* __restrict__ s3;   // cnee.xyz, Le0.z
+  float4* __restrict__ s4;   // cmed.xyz, -
+  uint4* __restrict__ s5;    // wseed, bounce, flags, -
+  float4* __restrict__ ro;   // continuation ray origin (xyz)
+  float4* __restrict__ rd;   // continuation ray direction
+  float4* __restrict__ so;   // shadow ray origin
+  float4* __restrict__ sd;   // shadow ray direction
+  int2* __restrict__ res;    // per path: [2*p + 0] continuation (tri, t bits), [2*p + 1] shadow
+  float4* __restrict__ fin;  // per path: final radiance curColor (RT:1549) awaiting the blend
+  const unsigned int* __restrict__ pix_xy;   // per work item: px | py << 16
+  const unsigned int* __restrict__ pix_acc;  // per work item: accumulation index
+  int* queue[2];                // ray queue entries: path << 1 | is_shadow
+  int* active[2];               // active path ids
+  unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
+};
+
+struct WFParams {
+  KParams K;  // scene, env, camera, frame geometry; K.n_work = valid pixels of this rank
+  WFState S;
+  int n_frames;  // frames in flight: slots = n_frames * K.n_work
+  int pass;      // bounce pass: queue/active set pass&1 in, (pass+1)&1 out
+};
+
+// Map a work index of this rank to (pixel, accumulation index); false outside the frame.
+RTD bool work_pixel(const KParams& P, unsigned int w, int& px, int& py, int& accIdx) {
+  const int tpx = P.tile_w * P.tile_h;
+  int lt = (int)(w / (unsigned)tpx);
+  int r = (int)(w - (unsigned)lt * (unsigned)tpx);
+  int gt = P.rank + lt * P.world;
+  int tx = gt % P.tiles_x, ty = gt / P.tiles_x;
+  int blk = r >> 6, in = r & 63;
+  int bxs = P.tile_w >> 3;
+  int lx = (blk % bxs) * 8 + (in & 7);
+  int ly = (blk / bxs) * 8 + (in >> 3);
+  px = tx * P.tile_w + lx;
+  py = ty * P.tile_h + ly;
+  accIdx = lt * tpx + ly * P.tile_w + lx;
+  return px < P.W && py < P.H;
+}
+
+// wave-aggregated append of `want` lanes to a counter; returns this lane's slot
+RTD unsigned int wave_append(unsigned int* counter, bool want) {
+  const unsigned long long m = __ballot(want);
+  unsigned int base = 0;
+  if (m) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    if (lane == leader) base = atomicAdd(counter, (unsigned int)__popcll(m));
+    base = __shfl(base, leader);
+    base += (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
+  }
+  return base;
+}
+
+// Block-aggregated append: every thread of the block calls it (block-uniform control flow);
+// a thread appends `n` (0, 1 or 2) entries.  One global atomic per block (a single counter
+// word saturates near 88 atomics/us on MI355X, so per-wave or per-lane appends would
+// serialise a 2M-path pass).  Returns the thread's first slot.
+RTD unsigned int block_append(unsigned int* counter, unsigned int n, unsigned int* smem4 /* >= 5 uints */) {
+  const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+  const unsigned long long b1 = __ballot(n >= 1u), b2 = __ballot(n >= 2u);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const unsigned int mine = (unsigned int)(__popcll(b1 & below) + __popcll(b2 & below));
+  const unsigned int wtot = (unsigned int)(__popcll(b1) + __popcll(b2));
+  if (lane == 0) smem4[wave] = wtot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int acc = 0;
+    const int nw = (int)(blockDim.x >> 6);
+    for (int k = 0; k < nw; k++) { unsigned int t = smem4[k]; smem4[k] = acc; acc += t; }
+    smem4[4] = acc ? atomicAdd(counter, acc) : 0u;
+  }
+  __syncthreads();
+  const unsigned int slot = smem4[4] + smem4[wave] + mine;
+  __syncthreads();  // smem4 reused by the next call
+  return slot;
+}
+
+// ------------------------------------------------------------------------------- gen
+__global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
+  const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
+  const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
+  const unsigned int total = (unsigned)W.n_frames * P.n_work;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S.cnt[0] = total;  // queue 0 and active list 0 are the identity over all slots
+    S.cnt[2] = total;
+  }
+  for (unsigned int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
+    const unsigned int f = slot / P.n_work;
+    const unsigned int w = slot - f * P.n_work;
+    const unsigned int xy = S.pix_xy[w];
+    const int px = (int)(xy & 0xffffu), py = (int)(xy >> 16);
+    const float u = ((float)px + 0.5f) / (float)P.W;  // TexCoords (vertex_shader.glsl)
+    const float v = ((float)py + 0.5f) / (float)P.H;
+    const uint32_t wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * (u * v));  // R5
+    const f3 d = normalize(lbc + (u * 2.0f * P.half_w) * right + (v * 2.0f * P.half_h) * up);  // R6
+    S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
+    S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+    S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
+    S.queue[0][slot] = (int)(slot << 1);
+    S.active[0][slot] = (int)slot;
+  }
+}
+
+// progressive blend of the frames in flight, in frame order (RT:1552)
+__global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < P.n_work; w += gridDim.x * blockDim.x) {
+    const unsigned int ai = S.pix_acc[w];
+    const float4 h = P.accum[ai];
+    f3 acc = mk3(h.x, h.y, h.z);
+    for (int f = 0; f < W.n_frames; f++) {
+      const float4 c = S.fin[(size_t)f * P.n_work + w];
+      const int loopNum = P.loop_num[f];
+      const float n = (float)loopNum;
+      acc = (1.0f / n) * xyz(c) + ((float)(loopNum - 1) / n) * acc;
+    }
+    P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+  }
+}
+
+// ----------------------------------------------------------------------------- trace
+// Persistent traversal: every lane pulls queued rays one at a time (wave-aggregated atomics);
+// each loop iteration advances every busy lane by one internal node or one triangle.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const int qin = W.pass & 1;
+  const unsigned int nq = S.cnt[qin];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
+    S.cnt[qin ^ 1] = 0u;
+    S.cnt[2 + (qin ^ 1)] = 0u;
+  }
+  if (nq == 0u || !P.has_scene) {
+    if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
+      for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+        int e = S.queue[qin][i];
+        S.res[e] = make_int2(-1, 0);
+      }
+    }
+    return;
+  }
+  const int stride = blockDim.x;
+  const int K = P.stack_entries;
+  int* sref = reinterpret_cast<int*>(smem) + threadIdx.x;
+  float* sdist = reinterpret_cast<float*>(smem + (size_t)K * stride * 4) + threadIdx.x;
+  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
+
+  bool busy = false, anyhit = false, haveCur = false;
+  // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
+  unsigned int pool_next = 0, pool_end = 0;
+  bool drained = false;
+  const int lane = (int)(threadIdx.x & 63);
+  int entry = 0, sp = 0, cur = 0, tri_i = 0, tri_end = 0, besttri = -1;
+  float best = INF, bestt = 0.0f;
+  f3 o = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
+  unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
+
+  while (true) {
+    if (COUNT) v_iter++;
+    // ---- refill idle lanes from the wave's pool; one global atomic per 64 rays
+    const unsigned long long idle = __ballot(!busy);
+    if (idle && !drained) {
+      if (pool_next >= pool_end) {
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(&S.cnt[4], 64u);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+        if (base >= nq) {
+          drained = true;
+        } else {
+          pool_next = base;
+          pool_end = min(base + 64u, nq);
+        }
+      }
+      if (!drained || pool_next < pool_end) {
+        const unsigned int avail = pool_end - pool_next;
+        const unsigned int rank = (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
+        if (!busy && rank < avail) {
+          const unsigned int slot = pool_next + rank;
+          entry = S.queue[qin][slot];
+          const int path = entry >> 1;
+          anyhit = (entry & 1) != 0;
+          const float4 oo = anyhit ? S.so[path] : S.ro[path];
+          const float4 dd = anyhit ? S.sd[path] : S.rd[path];
+          o = mk3(oo.x, oo.y, oo.z);
+          d = mk3(dd.x, dd.y, dd.z);
+          inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+          best = INF;
+          besttri = -1;
+          bestt = 0.0f;
+          sp = 0;
+          cur = P.root;
+          haveCur = true;
+          tri_i = tri_end = 0;
+          busy = true;
+        }
+        pool_next += min((unsigned int)__popcll(idle), avail);
+      }
+    }
+    if (!__any(busy)) break;
+    if (busy) {
+      bool finished = false;
+      if (tri_i < tri_end) {
+        // ---------------- one triangle of the current leaf (RT:241-299, R1)
+        const int i = tri_i++;
+        if (COUNT) v_tri++;
+        const float4 A = P.tri[3 * i], B = P.tri[3 * i + 1], Cc = P.tri[3 * i + 2];
+        const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+        const f3 ng = mk3(A.w, B.w, Cc.w);
+        const float dn = dot(ng, d);
+        if (!(fabs_(dn) < 0.00001f)) {                              // RT:262
+          const float t = (dot(ng, p1) - dot(o, ng)) / dot(d, ng);  // RT:265
+          const float dist = t - 0.00001f;
+          if (t >= 0.0005f && dist < best) {                        // RT:268, RT:328/356
+            const f3 Pp = o + d * t;
+            const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
+            const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
+            const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
+            if ((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0)) {
+              best = dist;
+              besttri = i;
+              bestt = t;
+              if (anyhit) finished = true;
+            }
+          }
+        }
+      } else if (haveCur) {
+        if (ref_is_leaf(cur)) {
+          if (COUNT) v_leaf++;
+          tri_i = leaf_first(cur);
+          tri_end = tri_i + leaf_count(cur);
+          haveCur = false;
+        } else {
+          if (COUNT) v_int++;
+          const GNode nd = P.nodes[cur];
+          float e1, e2;
+          const float d1 = slab(o, inv, mk3(nd.b0.x, nd.b0.y, nd.b0.z), mk3(nd.b0.w, nd.b1.x, nd.b1.y), e1);
+          const float d2 = slab(o, inv, mk3(nd.b1.z, nd.b1.w, nd.b2.x), mk3(nd.b2.y, nd.b2.z, nd.b2.w), e2);
+          int nearRef = 0;
+          float nearE = 0.0f;
+          bool descend = false;
+          if (d1 > 0 && d2 > 0) {  // RT:373-382: near first, far stacked
+            const bool leftFirst = d1 < d2;
+            nearRef = leftFirst ? nd.ref.x : nd.ref.y;
+            nearE = leftFirst ? e1 : e2;
+            sref[sp * stride] = leftFirst ? nd.ref.y : nd.ref.x;
+            sdist[sp * stride] = leftFirst ? e2 : e1;
+            ++sp;
+            descend = true;
+          } else if (d1 > 0) {
+            nearRef = nd.ref.x; nearE = e1; descend = true;
+          } else if (d2 > 0) {
+            nearRef = nd.ref.y; nearE = e2; descend = true;
+          }
+          if (descend && cull && nearE > cull_limit(best)) descend = false;
+          cur = nearRef;
+          haveCur = descend;
+        }
+      }
+      if (!finished && !haveCur && tri_i >= tri_end) {
+        // pop the next surviving subtree (RT:348)
+        while (sp > 0) {
+          --sp;
+          const int r = sref[sp * stride];
+          const float dd = sdist[sp * stride];
+          if (cull && dd > cull_limit(best)) continue;
+          cur = r;
+          haveCur = true;
+          break;
+        }
+        if (!haveCur) finished = true;
+      }
+      if (finished) {
+        S.res[entry] = make_int2(besttri, __float_as_int(bestt));
+        busy = false;
+      }
+    }
+  }
+  if (COUNT) {
+    for (int off = 32; off > 0; off >>= 1) {
+      v_int += __shfl_xor(v_int, off);
+      v_leaf += __shfl_xor(v_leaf, off);
+      v_tri += __shfl_xor(v_tri, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&P.stats[2], v_int);
+      atomicAdd(&P.stats[3], v_leaf);
+      atomicAdd(&P.stats[4], v_tri);
+      atomicAdd(&P.stats[5], v_iter);
+      atomicMax(&P.stats[6], v_iter);
+    }
+  }
+}
+
+// Variant: every lane runs the complete traversal of its ray (the megakernel's trace()), then
+// the wave refills from its pool.  Selected with RT_FLAG_TRACE_WHOLE.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void wf_trace_whole(const WFParams W) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const int qin = W.pass & 1;
+  const unsigned int nq = S.cnt[qin];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S.cnt[qin ^ 1] = 0u;
+    S.cnt[2 + (qin ^ 1)] = 0u;
+  }
+  const int stride = blockDim.x;
+  const int K = P.stack_entries;
+  int* sref = reinterpret_cast<int*>(smem) + threadIdx.x;
+  float* sdist = reinterpret_cast<float*>(smem + (size_t)K * stride * 4) + threadIdx.x;
+  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
+  const int lane = (int)(threadIdx.x & 63);
+  Visits vis{0, 0, 0};
+  while (true) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&S.cnt[4], 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= nq) break;
+    const unsigned int slot = base + (unsigned)lane;
+    if (slot < nq) {
+      const int entry = S.queue[qin][slot];
+      const int path = entry >> 1;
+      const bool anyhit = (entry & 1) != 0;
+      const float4 oo = anyhit ? S.so[path] : S.ro[path];
+      const float4 dd = anyhit ? S.sd[path] : S.rd[path];
+      int besttri;
+      float bestt;
+      trace<COUNT>(P, mk3(oo.x, oo.y, oo.z), mk3(dd.x, dd.y, dd.z), anyhit, cull, sref, sdist, stride, besttri,
+                   bestt, vis);
+      S.res[entry] = make_int2(besttri, __float_as_int(bestt));
+    }
+  }
+  if (COUNT) {
+    for (int off = 32; off > 0; off >>= 1) {
+      vis.internal += __shfl_xor(vis.internal, off);
+      vis.leaf += __shfl_xor(vis.leaf, off);
+      vis.tri += __shfl_xor(vis.tri, off);
+    }
+    if (lane == 0) {
+      atomicAdd(&P.stats[2], vis.internal);
+      atomicAdd(&P.stats[3], vis.leaf);
+      atomicAdd(&P.stats[4], vis.tri);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- shade
+__global__ __launch_bounds__(256) void wf_shade(const WFParams W) {
+  __shared__ unsigned int sm[8];
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const int in = W.pass & 1, out = in ^ 1;
+  const unsigned int na = S.cnt[2 + in];
+  const unsigned int nq_in = S.cnt[in];
+  if (blockIdx.x == 0 && threadIdx.x == 0) S.cnt[4] = 0u;  // fetch counter of the next trace pass
+  const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+  unsigned long long nrays = 0, nsamples = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
+  for (unsigned int base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
+    const unsigned int idx = base + threadIdx.x;
+    const bool live = idx < na;
+    int path = live ? S.active[in][idx] : 0;
+    bool doFinish = false, doBounce = false;
+    bool qShadow = false, qCont = false;
+    f3 fin = splat(0.0f);
+    float4 a0 = make_float4(0, 0, 0, 0), a1 = a0, a2 = a0, a3 = a0, a4 = a0;
+    uint4 a5 = make_uint4(0, 0, 0, 0);
+    f3 hist = splat(1.0f), Lo = splat(0.0f), Le0 = splat(0.0f), evf = splat(0.0f);
+    float evp = 0.0f;
+    uint32_t wseed = 0, bounce = 0, flags = 0, frame = 0;
+    f3 hP = splat(0.0f), hN = splat(0.0f), hV = splat(0.0f);
+    float hDist = 0.0f;
+    int mat = 0;
+    if (live) {
+      a5 = S.s5[path];
+      wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
+      if (!(flags & PF_CAMERA)) {
+        a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path];
+        hist = xyz(a0); evp = a0.w;
+        Lo = xyz(a1);
+        evf = xyz(a2);
+        Le0 = mk3(a1.w, a2.w, 0.0f);
+        a3 = S.s3[path];
+        Le0.z = a3.w;
+        // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
+        if ((flags & PF_SHADOW) && S.res[2 * path + 1].x < 0) Lo = Lo + xyz(a3);
+        // ---- pending medium-emissive term (RT:1437-1439)
+        if (flags & PF_CMED) {
+          a4 = S.s4[path];
+          Lo = Lo + xyz(a4);
+        }
+      }
+      if (!(flags & PF_CONT)) {  // BSDF pdf was 0 (RT:1460-1462): the path ends
+        fin = Le0 + Lo;
+        doFinish = true;
+      } else {
+        const int2 r = S.res[2 * path];
+        const float4 oo = S.ro[path], dd = S.rd[path];
+        const f3 ro = xyz(oo), rd = xyz(dd);
+        if (r.x >= 0) {
+          const int tri = r.x;
+          const float t = __int_as_float(r.y);
+          const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
+          const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
+          const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+          const f3 ng = mk3(A.w, B.w, Cc.w);
+          const bool inside = dot(ng, rd) > 0.0f;
+          const f3 Pp = ro + rd * t;
+          const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
+                              (-(p1.x - p2.x) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
+          const float beta = (-(Pp.x - p3.x) * (p1.y - p3.y) + (Pp.y - p3.y) * (p1.x - p3.x)) /
+                             (-(p2.x - p3.x) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
+          const float gama = 1.0f - alpha - beta;
+          const f3 Ns = normalize(alpha * xyz(N1) + beta * xyz(N2) + gama * xyz(N3));
+          const int nmat = __float_as_int(N1.w);
+          if (flags & PF_CAMERA) {  // RT:1541-1544
+            Le0 = xyz(P.mats[8 * nmat]);
+            Lo = splat(0.0f);
+            hist = splat(1.0f);
+            bounce = 0;
+          } else {  // RT:1509-1510
+            const f3 Le = xyz(P.mats[8 * nmat]);
+            Lo = Lo + hist * Le * evf / evp;
+            bounce++;
+          }
+          hP = Pp;
+          hN = inside ? -Ns : Ns;
+          hV = rd;
+          hDist = t - 0.00001f;
+          mat = nmat;
+          if ((int)bounce < P.max_bounce) doBounce = true;
+          else { fin = Le0 + Lo; doFinish = true; }
+        } else if (flags & PF_CAMERA) {  // RT:1532-1539
+          fin = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
+          doFinish = true;
+        } else {  // RT:1483-1506
+          if (P.enable_env) {
+            f3 light_fr;
+            float light_pdf;
+            hdrColorPdf(E, rd, light_fr, light_pdf);
+            light_fr = light_fr * E.intensity;
+            float mis_weight = misMixWeight(evp, light_pdf);
+            if (!P.enable_mis) mis_weight = 1.0f;
+            if (!(flags & PF_MEDIUM)) Lo = Lo + mis_weight * hist * light_fr * evf / evp;
+            else Lo = Lo + hist * light_fr * evf / light_pdf;
+          } else {
+            const f3 light_fr = getDefaultSkyColor(rd.y);
+            Lo = Lo + hist * light_fr * evf / evp;
+          }
+          fin = Le0 + Lo;
+          doFinish = true;
+        }
+      }
+    }
+
+    // ------------------------------------------------------------- next bounce
+    f3 cnee = splat(0.0f), cmed = splat(0.0f);
+    uint32_t nflags = 0;
+    f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
+    if (doBounce) {
+      const Mat m = load_mat(P.mats, mat);
+      const f3 V = -hV;
+      // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
+      const float xa = rand_(wseed);  // R24
+      const float xb = rand_(wseed);
+      const f3 Ll = SampleHdr(E, xa, xb);
+      if (dot(hN, Ll) > 0.0f) {
+        f3 light_fr;
+        float light_pdf;
+        hdrColorPdf(E, Ll, light_fr, light_pdf);
+        light_fr = light_fr * E.intensity;
+        float disney_eval_pdf;
+        const f3 disney_eval_fr = DisneyEval(m, V, hN, Ll, disney_eval_pdf);
+        float mis_weight = misMixWeight(light_pdf, disney_eval_pdf);
+        if (!P.enable_mis) mis_weight = 1.0f;
+        cnee = mis_weight * hist * light_fr * disney_eval_fr / light_pdf;
+        shO = hP;
+        shD = Ll;
+        qShadow = true;
+        nflags |= PF_SHADOW;
+      }
+      // BSDF sample (RT:1408-1474)
+      int g = P.loop_num[frame] + 1;
+      g = g ^ (g >> 1);
+      float sx = sobol_gray((int)bounce * 2, g);
+      float sy = sobol_gray((int)bounce * 2 + 1, g);
+      const float cu = rand_(wseed), cv = rand_(wseed);
+      sx += cu;
+      if (sx > 1) sx -= 1;
+      if (sx < 0) sx += 1;
+      sy += cv;
+      if (sy > 1) sy -= 1;
+      if (sy < 0) sy += 1;
+      const float xi_3 = rand_(wseed);
+      f3 L;
+      float pdf;
+      bool isRefract;
+      const f3 fr = DisneySample(sx, sy, xi_3, m, V, hN, L, pdf, isRefract);
+      bool medS = false;
+      float scatter_pdf = 0.0f;
+      float transmittance = 1.0f;
+      if (pdf > 0.0f) {
+        if (!isRefract) {
+          hist = hist * (fr / pdf);
+        } else if (m.mtype == MEDIUM_ABSORB) {
+          hist = hist * exp3(-(splat(1.0f) - m.mcolor) * hDist * m.mdensity);
+        } else if (m.mtype == MEDIUM_EMISSIVE) {
+          cmed = m.mcolor * hDist * m.mdensity * hist;
+          nflags |= PF_CMED;
+        } else if (m.mtype == MEDIUM_SCATTER) {
+          const float scatterDist = min_(-log_(xi_3) / m.mdensity, hDist);
+          medS = scatterDist < hDist;
+          if (medS) {
+            transmittance *= exp_(-1.0f * scatterDist);
+            hist = hist * (m.mcolor * transmittance);
+            hP = hP + hV * scatterDist;
+            const f3 scatterDir = SampleHG(V, m.manis, sx, sy);
+            scatter_pdf = PhaseHG(dot(V, scatterDir), m.manis);
+            L = scatterDir;
+          }
+        }
+        evf = DisneyEval(m, V, hN, L, evp);
+        if (medS && scatter_pdf > 0.0f) {
+          evp = scatter_pdf;
+          evf = splat(scatter_pdf);
+        }
+        if (medS) nflags |= PF_MEDIUM;
+        contO = hP;
+        contD = L;
+        qCont = true;
+        nflags |= PF_CONT;
+      }
+      if (!qShadow && !qCont) {  // no ray left: finish now (RT:1460-1462 break)
+        fin = Le0 + Lo;
+        doFinish = true;
+      }
+    }
+
+    // ----------------------------------------------------------- progressive blend
+    if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
+      S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
+      nsamples++;
+    }
+
+    // ------------------------------------------------------------ enqueue rays
+    const bool keep = qShadow || qCont;
+    if (keep) {
+      S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
+      S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
+      S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
+      S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
+      if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
+      S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
+      if (qCont) {
+        S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
+        S.rd[path] = make_float4(contD.x, contD.y, contD.z, 0.0f);
+      }
+      if (qShadow) {
+        S.so[path] = make_float4(shO.x, shO.y, shO.z, 0.0f);
+        S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
+      }
+    }
+    const unsigned int qs = block_append(&S.cnt[out], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u), sm);
+    if (qShadow) S.queue[out][qs] = (path << 1) | 1;
+    if (qCont) S.queue[out][qs + (qShadow ? 1u : 0u)] = path << 1;
+    const unsigned int ai = block_append(&S.cnt[2 + out], keep ? 1u : 0u, sm);
+    if (keep) S.active[out][ai] = path;
+  }
+  // per-wave counter flush
+  for (int off = 32; off > 0; off >>= 1) {
+    nrays += __shfl_xor(nrays, off);
+    nsamples += __shfl_xor(nsamples, off);
+  }
+  if ((threadIdx.x & 63) == 0 && (nrays | nsamples)) {
+    atomicAdd(&P.stats[0], nrays);
+    atomicAdd(&P.stats[1], nsamples);
+  }
+}
+
+}  // namespace rtd

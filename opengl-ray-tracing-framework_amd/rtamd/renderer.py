@@ -20,6 +20,7 @@ RT_OK, RT_ERR_ARG, RT_ERR_HIP, RT_ERR_STATE, RT_ERR_NOMEM, RT_ERR_NODEVICE, RT_E
 RT_MAX_FRAMES_PER_LAUNCH = 64
 RT_FLAG_NO_CULL = 1
 RT_FLAG_COUNT_VISITS = 2
+RT_FLAG_MEGAKERNEL = 4
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 
 _f32p = C.POINTER(C.c_float)
@@ -72,7 +73,8 @@ class RtFrameParams(C.Structure):
 class RtStats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("samples", C.c_uint64), ("internal_pops", C.c_uint64),
                 ("leaf_pops", C.c_uint64), ("tri_tests", C.c_uint64), ("launches", C.c_uint64),
-                ("kernel_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("trace_launches", C.c_uint64), ("trace_ms", C.c_double),
+                ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

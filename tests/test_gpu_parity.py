@@ -11,16 +11,17 @@ import pytest
 
 from helpers import bit_mismatch, frames_for, gpu_render, oracle_render
 from rtamd import configs as cf
-from rtamd.renderer import RT_FLAG_NO_CULL
+from rtamd.renderer import RT_FLAG_MEGAKERNEL, RT_FLAG_NO_CULL
 
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("flags", [0, RT_FLAG_MEGAKERNEL], ids=["wavefront", "megakernel"])
 @pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
-def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name):
+def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     sd = cf.config_scene(name)
     W, H = 96, 54
-    fp = cf.frame_params(W, H)
+    fp = cf.frame_params(W, H, flags=flags)
     ro, frames = frames_for(fp, 1, 2)
     ref, cnt = oracle_render(sd, env_maps, W, H, frames)
     img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
@@ -48,3 +49,19 @@ def test_encoded_aos_entry_point(gpu_renderer, env_maps):
     ref, _ = oracle_render(sd, env_maps, W, H, frames)
     img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro, encoded=True)
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_maps, monkeypatch):
+    """Frames in flight are blended in frame order: 1 frame per wavefront (tiny path-state
+    budget) and all frames at once give the same bits, and both equal the oracle."""
+    sd = cf.config_scene("C3")
+    W, H = 64, 36
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 3)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    monkeypatch.setenv("RT_MAX_SLOTS", str(W * H))  # -> one frame in flight
+    img1, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    monkeypatch.delenv("RT_MAX_SLOTS")
+    img3, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert bit_mismatch(img1, ref)[0] == 0.0
+    assert bit_mismatch(img3, ref)[0] == 0.0

@@ -17,6 +17,8 @@ ap.add_argument("--frames", type=int, default=4)
 ap.add_argument("--per-launch", type=int, default=1)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
+ap.add_argument("--max-bounce", type=int, default=8)
+ap.add_argument("--flags", type=int, default=0)
 a = ap.parse_args()
 cfg = cf.CONFIGS[a.config]
 W, H = a.width or cfg.width, a.height or cfg.height
@@ -29,7 +31,7 @@ r.set_scene_soa(sd.soa, sd.nodes)
 r.set_env(*env)
 r.resize(W, H)
 print("device", r.device_info(), flush=True)
-fp = cf.frame_params(W, H)
+fp = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=a.flags)
 ro = cf.rand_origins(a.frames + 1 + 64)
 r.render(fp, ro[:1])
 r.reset_stats()
@@ -42,11 +44,13 @@ while k < a.frames + 1:
 st = r.stats()
 wall = time.time() - t
 ms = st["kernel_ms"] / a.frames
-print(f"{a.config} {W}x{H}: {ms:.2f} ms/frame (kernel), wall {wall*1000/a.frames:.2f} ms/frame, "
+print(f"{a.config} {W}x{H} mb={a.max_bounce} flags={a.flags}: {ms:.2f} ms/frame (kernel), wall {wall*1000/a.frames:.2f} ms/frame, "
       f"{st['rays']/st['kernel_ms']/1e3:.1f} Mrays/s, rays/frame {st['rays']/a.frames/1e6:.2f} M", flush=True)
-fpc = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS)
+fpc = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=RT_FLAG_COUNT_VISITS | a.flags)
 r.reset_stats()
 r.render(fpc, ro[-1:])
 st = r.stats()
-print("visits per ray: internal %.1f leaf %.1f tri %.1f" % (st["internal_pops"] / st["rays"],
-      st["leaf_pops"] / st["rays"], st["tri_tests"] / st["rays"]), flush=True)
+print("visits per ray: internal %.1f leaf %.1f tri %.1f; trace loop iters/wave-pass avg %.0f max %d (%d launches)" % (
+      st["internal_pops"] / st["rays"], st["leaf_pops"] / st["rays"], st["tri_tests"] / st["rays"],
+      st["trace_iters"] / max(1, st["trace_launches"]) / 3072, st["trace_iters_max"], st["trace_launches"]), flush=True)
+
