@@ -93,8 +93,7 @@ typedef struct rt_frame_params {
 enum {
   RT_FLAG_NO_CULL = 1,            /* disable closest-hit box culling (exhaustive RT:338 order)  */
   RT_FLAG_COUNT_VISITS = 2,       /* also count node/triangle visits (slower)                  */
-  RT_FLAG_MEGAKERNEL = 4,         /* single persistent megakernel instead of the wavefront path */
-  RT_FLAG_TRACE_WHOLE = 8         /* wavefront traversal: whole ray per lane between refills    */
+  RT_FLAG_MEGAKERNEL = 4          /* single persistent megakernel instead of the wavefront path */
 };
 
 typedef struct rt_stats {

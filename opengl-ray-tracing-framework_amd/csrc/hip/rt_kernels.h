@@ -39,6 +39,9 @@ struct KParams {
   unsigned int n_work;
   const GNode* __restrict__ nodes;
   int root, has_scene, stack_entries;
+  int lds_entries;                  // wavefront traversal: stack entries kept in LDS
+  int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]
+  unsigned int ovf_lanes;
   const float4* __restrict__ tri;   // 3 per triangle: {p1, Ng.x} {p2, Ng.y} {p3, Ng.z}
   const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, 0} {n3, 0}
   const float4* __restrict__ mats;  // 8 per material

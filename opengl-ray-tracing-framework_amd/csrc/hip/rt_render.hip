@@ -56,6 +56,9 @@ struct rt_ctx {
   uint64_t launches = 0, trace_launches = 0;
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0;                          // wavefront traversal kernel
+  int trace_lds_entries = 0, trace_lds = 0;
+  int2* d_stack_ovf = nullptr;
+  size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
   void* wf_mem = nullptr;
   size_t wf_paths = 0;
@@ -119,9 +122,22 @@ int occupancy(rt_ctx* c) {
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::rt_path_kernel<false>, 256, lds));
   c->blocks_per_cu = std::max(1, bpc);
   c->block_lds = lds;
+  // wavefront traversal: short LDS stack + global overflow
+  int kl = 12;
+  if (const char* e = getenv("RT_LDS_STACK")) kl = atoi(e);
+  kl = std::max(1, std::min(kl, c->stack_entries));
+  c->trace_lds_entries = kl;
+  c->trace_lds = kl * 256 * 8;
   bpc = 0;
-  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false>, 256, lds));
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false>, 256, c->trace_lds));
   c->trace_bpc = std::max(1, bpc);
+  const size_t lanes = (size_t)c->n_cus * c->trace_bpc * 256;
+  const size_t need = (size_t)std::max(0, c->stack_entries - kl) * lanes * sizeof(int2);
+  if (need > c->stack_ovf_bytes) {
+    dfree(c->d_stack_ovf);
+    HIPCHK(c, hipMalloc(&c->d_stack_ovf, need));
+    c->stack_ovf_bytes = need;
+  }
   return RT_OK;
 }
 
@@ -197,6 +213,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   dfree(c->d_pix);
+  dfree(c->d_stack_ovf);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -540,9 +557,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const unsigned int slots = (unsigned)nf * (unsigned)c->n_valid;
       const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots + 255) / 256));
       const unsigned int shade_grid = gen_grid;
-      unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
-      if (const char* g = getenv("RT_TRACE_GRID")) trace_grid = (unsigned)atoi(g);  // experiments
-      const bool whole = (fp->flags & RT_FLAG_TRACE_WHOLE) != 0;
+      const unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
+      WP.K.lds_entries = c->trace_lds_entries;
+      WP.K.stack_ovf = c->d_stack_ovf;
+      WP.K.ovf_lanes = trace_grid * 256u;
       HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));
       WP.pass = 0;
       hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, c->stream, WP);
@@ -552,14 +570,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         hipEvent_t t0 = take_event(c), t1 = take_event(c);
         if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
         HIPCHK(c, hipEventRecord(t0, c->stream));
-        if (count && whole)
-          hipLaunchKernelGGL(rtd::wf_trace_whole<true>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
-        else if (whole)
-          hipLaunchKernelGGL(rtd::wf_trace_whole<false>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
-        else if (count)
-          hipLaunchKernelGGL(rtd::wf_trace<true>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+        if (count)
+          hipLaunchKernelGGL(rtd::wf_trace<true>, dim3(trace_grid), dim3(256), c->trace_lds, c->stream, WP);
         else
-          hipLaunchKernelGGL(rtd::wf_trace<false>, dim3(trace_grid), dim3(256), c->block_lds, c->stream, WP);
+          hipLaunchKernelGGL(rtd::wf_trace<false>, dim3(trace_grid), dim3(256), c->trace_lds, c->stream, WP);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(t1, c->stream));
         c->trace_events.push_back({t0, t1});

@@ -189,9 +189,13 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
     return;
   }
   const int stride = blockDim.x;
-  const int K = P.stack_entries;
-  int* sref = reinterpret_cast<int*>(smem) + threadIdx.x;
-  float* sdist = reinterpret_cast<float*>(smem + (size_t)K * stride * 4) + threadIdx.x;
+  // traversal stack: the top lds_entries entries of every lane in LDS ([entry][lane], 8-B
+  // {ref, entry distance} pairs, conflict-free ds_read/write_b64), deeper entries in a global
+  // overflow region ([entry][grid lane], coalesced) that only very deep stacks touch.
+  const int KL = P.lds_entries;
+  int2* slds = reinterpret_cast<int2*>(smem) + threadIdx.x;
+  int2* sovf = P.stack_ovf + (blockIdx.x * blockDim.x + threadIdx.x);
+  const unsigned int ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
 
   bool busy = false, anyhit = false, haveCur = false;
@@ -291,8 +295,9 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
             const bool leftFirst = d1 < d2;
             nearRef = leftFirst ? nd.ref.x : nd.ref.y;
             nearE = leftFirst ? e1 : e2;
-            sref[sp * stride] = leftFirst ? nd.ref.y : nd.ref.x;
-            sdist[sp * stride] = leftFirst ? e2 : e1;
+            const int2 ent = make_int2(leftFirst ? nd.ref.y : nd.ref.x, __float_as_int(leftFirst ? e2 : e1));
+            if (sp < KL) slds[sp * stride] = ent;
+            else sovf[(size_t)(sp - KL) * ovs] = ent;
             ++sp;
             descend = true;
           } else if (d1 > 0) {
@@ -309,10 +314,9 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
         // pop the next surviving subtree (RT:348)
         while (sp > 0) {
           --sp;
-          const int r = sref[sp * stride];
-          const float dd = sdist[sp * stride];
-          if (cull && dd > cull_limit(best)) continue;
-          cur = r;
+          const int2 ent = sp < KL ? slds[sp * stride] : sovf[(size_t)(sp - KL) * ovs];
+          if (cull && __int_as_float(ent.y) > cull_limit(best)) continue;
+          cur = ent.x;
           haveCur = true;
           break;
         }
@@ -336,59 +340,6 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
       atomicAdd(&P.stats[4], v_tri);
       atomicAdd(&P.stats[5], v_iter);
       atomicMax(&P.stats[6], v_iter);
-    }
-  }
-}
-
-// Variant: every lane runs the complete traversal of its ray (the megakernel's trace()), then
-// the wave refills from its pool.  Selected with RT_FLAG_TRACE_WHOLE.
-template <bool COUNT>
-__global__ __launch_bounds__(256) void wf_trace_whole(const WFParams W) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const KParams& P = W.K;
-  const WFState& S = W.S;
-  const int qin = W.pass & 1;
-  const unsigned int nq = S.cnt[qin];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S.cnt[qin ^ 1] = 0u;
-    S.cnt[2 + (qin ^ 1)] = 0u;
-  }
-  const int stride = blockDim.x;
-  const int K = P.stack_entries;
-  int* sref = reinterpret_cast<int*>(smem) + threadIdx.x;
-  float* sdist = reinterpret_cast<float*>(smem + (size_t)K * stride * 4) + threadIdx.x;
-  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
-  const int lane = (int)(threadIdx.x & 63);
-  Visits vis{0, 0, 0};
-  while (true) {
-    unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(&S.cnt[4], 64u);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-    if (base >= nq) break;
-    const unsigned int slot = base + (unsigned)lane;
-    if (slot < nq) {
-      const int entry = S.queue[qin][slot];
-      const int path = entry >> 1;
-      const bool anyhit = (entry & 1) != 0;
-      const float4 oo = anyhit ? S.so[path] : S.ro[path];
-      const float4 dd = anyhit ? S.sd[path] : S.rd[path];
-      int besttri;
-      float bestt;
-      trace<COUNT>(P, mk3(oo.x, oo.y, oo.z), mk3(dd.x, dd.y, dd.z), anyhit, cull, sref, sdist, stride, besttri,
-                   bestt, vis);
-      S.res[entry] = make_int2(besttri, __float_as_int(bestt));
-    }
-  }
-  if (COUNT) {
-    for (int off = 32; off > 0; off >>= 1) {
-      vis.internal += __shfl_xor(vis.internal, off);
-      vis.leaf += __shfl_xor(vis.leaf, off);
-      vis.tri += __shfl_xor(vis.tri, off);
-    }
-    if (lane == 0) {
-      atomicAdd(&P.stats[2], vis.internal);
-      atomicAdd(&P.stats[3], vis.leaf);
-      atomicAdd(&P.stats[4], vis.tri);
     }
   }
 }
