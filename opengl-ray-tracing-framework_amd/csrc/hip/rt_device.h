@@ -66,6 +66,15 @@ struct __attribute__((aligned(16))) GNode {
   float4 b2;  // R.AA.z,   R.BB.xyz
   int4 ref;   // left ref, right ref, -, -
 };
+// 4-wide node collapsed from the binary tree above (same exact fp32 child boxes, SoA: child k
+// in component k; an empty slot has NaN bounds, which the slab test never hits).  128 B = one
+// cache line; one fetch replaces about two dependent binary steps.
+struct __attribute__((aligned(16))) QNode {
+  float4 lox, loy, loz, hix, hiy, hiz;
+  int4 ref;  // child refs (QNode index or leaf ref), Q_EMPTY for an empty slot
+  int4 pad;
+};
+constexpr int Q_EMPTY = 0x7fffffff;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 RTD bool ref_is_leaf(int r) { return ((uint32_t)r & LEAF_BIT) != 0u; }
 RTD int leaf_first(int r) { return (int)(((uint32_t)r & 0x7fffffffu) >> 4); }

@@ -37,13 +37,15 @@ struct KParams {
   float rand_origin[RT_MAX_FRAMES_PER_LAUNCH];
   int W, H, tile_w, tile_h, tiles_x, rank, world;
   unsigned int n_work;
-  const GNode* __restrict__ nodes;
+  const GNode* __restrict__ nodes;  // binary tree; GNode.ref.z = DFS rank of the first leaf on the right
   int root, has_scene, stack_entries;
+  const QNode* __restrict__ qnodes;  // 4-wide collapse of `nodes` (wavefront trace, TW_WIDE)
+  int qroot;
   int lds_entries;                  // wavefront traversal: stack entries kept in LDS
   int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]
   unsigned int ovf_lanes;
   const float4* __restrict__ tri;   // 3 per triangle: {p1, Ng.x} {p2, Ng.y} {p3, Ng.z}
-  const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, 0} {n3, 0}
+  const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, leaf rank bits} {n3, 0}
   const float4* __restrict__ mats;  // 8 per material
   const float4* __restrict__ hdr;
   const float4* __restrict__ cache;

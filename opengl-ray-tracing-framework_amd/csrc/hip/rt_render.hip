@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
+#include <functional>
 #include <new>
 #include <string>
 #include <vector>
@@ -28,6 +30,9 @@ struct rt_ctx {
   std::string err;
   // scene
   GNode* d_nodes = nullptr;
+  rtd::QNode* d_qnodes = nullptr;
+  int qroot = 0, qstack_entries = 2;
+  bool wide = false;                          // 4-wide traversal available for this scene
   float4* d_tri = nullptr;
   float4* d_trin = nullptr;
   float4* d_mats = nullptr;
@@ -57,6 +62,7 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0;                          // wavefront traversal kernel
   int trace_lds_entries = 0, trace_lds = 0;
+  int trace_mode = 0;                         // rtd::TraceMode
   int2* d_stack_ovf = nullptr;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
@@ -108,6 +114,101 @@ void pack_material(const rt_material& m, float* o) {
   o[27] = o[28] = o[29] = o[30] = o[31] = 0.0f;
 }
 
+// Leaf ranks + 4-wide collapse of the binary tree.
+// * Leaf rank = position of the leaf in the reference's left-first DFS; gn[k].ref.z = rank of
+//   the first leaf of node k's right subtree; trin[3t+1].w = rank of triangle t's leaf.  These
+//   let the 4-wide traversal break exact distance ties the way the reference's visit order does.
+// * A QNode replaces a binary node and up to two levels below it: its slots start as the two
+//   children and the internal slot with the largest surface area is split until there are 4.
+//   Boxes are copied bit for bit.  A (grand)child box can only be hit when every box above it is
+//   (children are min/max over subsets, and the slab arithmetic is monotone), so the 4-wide
+//   traversal reaches exactly the reference's leaves.
+// Returns false (binary traversal only) when a triangle belongs to two leaves.
+bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std::vector<rtd::QNode>& qn,
+                int& qroot, int& qdepth) {
+  const int nt = (int)(trin.size() / 3);
+  auto is_leaf = [](int r) { return ((uint32_t)r & rtd::LEAF_BIT) != 0u; };
+  auto first_of = [](int r) { return (int)(((uint32_t)r & 0x7fffffffu) >> 4); };
+  auto count_of = [](int r) { return (int)((uint32_t)r & 15u) + 1; };
+  std::vector<int> tri_rank(nt, -1);
+  int rank = 0;
+  bool ok = true;
+  std::function<void(int)> rank_dfs = [&](int r) {
+    if (is_leaf(r)) {
+      for (int t = first_of(r); t < first_of(r) + count_of(r); t++) {
+        if (tri_rank[t] >= 0) ok = false;
+        tri_rank[t] = rank;
+      }
+      rank++;
+      return;
+    }
+    rank_dfs(gn[r].ref.x);
+    gn[r].ref.z = rank;
+    rank_dfs(gn[r].ref.y);
+  };
+  rank_dfs(root);
+  for (int t = 0; t < nt; t++) {
+    float w;
+    memcpy(&w, &tri_rank[t], 4);
+    trin[3 * t + 1].w = w;
+  }
+  if (!ok) return false;
+  struct Slot {
+    int ref;
+    float lo[3], hi[3];
+  };
+  auto kids = [&](int b, Slot& L, Slot& R) {
+    const GNode& g = gn[b];
+    L = Slot{g.ref.x, {g.b0.x, g.b0.y, g.b0.z}, {g.b0.w, g.b1.x, g.b1.y}};
+    R = Slot{g.ref.y, {g.b1.z, g.b1.w, g.b2.x}, {g.b2.y, g.b2.z, g.b2.w}};
+  };
+  auto area = [](const Slot& s) {
+    double e[3];
+    for (int k = 0; k < 3; k++) e[k] = (double)s.hi[k] - (double)s.lo[k];
+    return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+  };
+  qdepth = 1;
+  std::function<int(int, int)> build = [&](int b, int depth) -> int {
+    qdepth = std::max(qdepth, depth);
+    const int idx = (int)qn.size();
+    qn.push_back(rtd::QNode{});
+    std::vector<Slot> sl(2);
+    kids(b, sl[0], sl[1]);
+    while (sl.size() < 4) {
+      int pick = -1;
+      double pa = -1.0;
+      for (size_t i = 0; i < sl.size(); i++)
+        if (!is_leaf(sl[i].ref) && area(sl[i]) > pa) { pa = area(sl[i]); pick = (int)i; }
+      if (pick < 0) break;
+      Slot x, y;
+      kids(sl[pick].ref, x, y);
+      sl[pick] = x;
+      sl.insert(sl.begin() + pick + 1, y);
+    }
+    int refs[4] = {rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY};
+    for (size_t i = 0; i < sl.size(); i++) refs[i] = is_leaf(sl[i].ref) ? sl[i].ref : build(sl[i].ref, depth + 1);
+    const float qnan = std::nanf("");
+    float lo[3][4], hi[3][4];
+    for (int k = 0; k < 3; k++)
+      for (int i = 0; i < 4; i++) {
+        lo[k][i] = i < (int)sl.size() ? sl[i].lo[k] : qnan;
+        hi[k][i] = i < (int)sl.size() ? sl[i].hi[k] : qnan;
+      }
+    rtd::QNode& q = qn[idx];
+    q.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    q.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    q.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    q.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    q.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    q.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    q.ref = make_int4(refs[0], refs[1], refs[2], refs[3]);
+    q.pad = make_int4((int)sl.size(), 0, 0, 0);
+    return idx;
+  };
+  qroot = is_leaf(root) ? root : build(root, 1);
+  return true;
+}
+
 int upload(rt_ctx* c, void** dst, const void* src, size_t bytes) {
   if (*dst) { (void)hipFree(*dst); *dst = nullptr; }
   if (bytes == 0) return RT_OK;
@@ -125,20 +226,49 @@ int occupancy(rt_ctx* c) {
   // wavefront traversal: short LDS stack + global overflow
   int kl = 12;
   if (const char* e = getenv("RT_LDS_STACK")) kl = atoi(e);
-  kl = std::max(1, std::min(kl, c->stack_entries));
+  kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
   bpc = 0;
-  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false>, 256, c->trace_lds));
+  c->trace_mode = rtd::TM_SPEC;
+  if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode = std::max(0, std::min(2, atoi(e)));
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256,
+                                                         c->trace_lds));
   c->trace_bpc = std::max(1, bpc);
   const size_t lanes = (size_t)c->n_cus * c->trace_bpc * 256;
-  const size_t need = (size_t)std::max(0, c->stack_entries - kl) * lanes * sizeof(int2);
+  const int entries = std::max(c->stack_entries, c->qstack_entries);
+  const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2);
   if (need > c->stack_ovf_bytes) {
     dfree(c->d_stack_ovf);
     HIPCHK(c, hipMalloc(&c->d_stack_ovf, need));
     c->stack_ovf_bytes = need;
   }
   return RT_OK;
+}
+
+template <bool COUNT, bool WIDE>
+void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP) {
+  switch (c->trace_mode) {
+    case rtd::TM_IFIF:
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_IFIF, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+      break;
+    case rtd::TM_WW:
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_WW, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+      break;
+    default:
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_SPEC, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+  }
+}
+
+template <bool COUNT>
+void launch_trace_t(rt_ctx* c, dim3 grid, const rtd::WFParams& WP) {
+  if (c->wide) launch_trace_w<COUNT, true>(c, grid, WP);
+  else launch_trace_w<COUNT, false>(c, grid, WP);
+}
+
+void launch_trace(rt_ctx* c, bool count, dim3 grid, const rtd::WFParams& WP) {
+  if (count) launch_trace_t<true>(c, grid, WP);
+  else launch_trace_t<false>(c, grid, WP);
 }
 
 hipEvent_t take_event(rt_ctx* c) {
@@ -155,7 +285,11 @@ hipEvent_t take_event(rt_ctx* c) {
 // Path-state buffers of the wavefront path, carved from one allocation.
 int alloc_wavefront(rt_ctx* c, size_t paths) {
   if (c->wf_mem && c->wf_paths >= paths) return RT_OK;
-  if (c->wf_mem) { (void)hipFree(c->wf_mem); c->wf_mem = nullptr; }
+  if (c->wf_mem) {  // grow: earlier launches on the stream may still read the old state
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(c->wf_mem);
+    c->wf_mem = nullptr;
+  }
   const size_t P = std::max<size_t>(paths, 64);
   const size_t bytes = P * (6 * 16 + 4 * 16 + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
   HIPCHK(c, hipMalloc(&c->wf_mem, bytes));
@@ -207,7 +341,7 @@ int rt_destroy(rt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
-  dfree(c->d_nodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
+  dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
   dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
@@ -317,12 +451,19 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
     }
     has = 1;
   }
+  std::vector<rtd::QNode> qn;
+  int qroot = root, qdepth = 1;
+  bool wide = false;
+  if (has) wide = build_wide(gn, root, trin, qn, qroot, qdepth);
+  if (const char* e = getenv("RT_BVH_WIDTH")) if (atoi(e) == 2) wide = false;
   if (gn.empty()) {
     GNode z;
     memset(&z, 0, sizeof(z));
     gn.push_back(z);
   }
+  if (qn.empty()) qn.push_back(rtd::QNode{});
   int rc;
+  if ((rc = upload(c, (void**)&c->d_qnodes, qn.data(), qn.size() * sizeof(rtd::QNode)))) return rc;
   if ((rc = upload(c, (void**)&c->d_nodes, gn.data(), gn.size() * sizeof(GNode)))) return rc;
   if ((rc = upload(c, (void**)&c->d_tri, tri.data(), tri.size() * sizeof(float4)))) return rc;
   if ((rc = upload(c, (void**)&c->d_trin, trin.data(), trin.size() * sizeof(float4)))) return rc;
@@ -332,6 +473,9 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
   c->root = root;
   c->has_scene = has;
   c->stack_entries = std::max(2, depth + 1);
+  c->wide = wide;
+  c->qroot = qroot;
+  c->qstack_entries = std::max(2, 3 * qdepth + 2);
   c->tri_mat.assign(s->material_id, s->material_id + nt);
   c->mat_table = mt;
   c->scene_set = true;
@@ -463,10 +607,12 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
   }
-  size_t max_slots = 8u << 20;  // ~1.8 GB of path state
+  // frames in flight: path-state budget of 64M slots (216 B each, ~14 GB of the 288 GB HBM);
+  // the state grows on demand in rt_render_async, so interactive 1-frame use stays small
+  size_t max_slots = size_t(1) << 26;
   if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
   c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / nv));
-  int rc = alloc_wavefront(c, (size_t)c->frames_cap * nv);
+  int rc = alloc_wavefront(c, nv);
   if (rc) return rc;
   c->wf.pix_xy = c->d_pix;
   c->wf.pix_acc = c->d_pix + nv;
@@ -503,6 +649,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   if (!c || !fp || n_frames < 0 || (n_frames && !rand_origin)) return RT_ERR_ARG;
   if (!c->scene_set || !c->env_set || !c->frame_set) return fail(c, RT_ERR_STATE, "set_scene, set_env and resize first");
   HIPCHK(c, hipSetDevice(c->device));
+  if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
+    const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
+    const int rc = alloc_wavefront(c, (size_t)std::min(c->frames_cap, (int)n_frames) * nv);
+    if (rc) return rc;
+  }
   int done = 0;
   while (done < n_frames) {
     KParams P;
@@ -530,6 +681,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.rank = c->rank; P.world = c->world;
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
+    P.qnodes = c->d_qnodes; P.qroot = c->qroot;
     P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
     P.hdr = c->d_hdr; P.cache = c->d_cache; P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
@@ -570,10 +722,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         hipEvent_t t0 = take_event(c), t1 = take_event(c);
         if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
         HIPCHK(c, hipEventRecord(t0, c->stream));
-        if (count)
-          hipLaunchKernelGGL(rtd::wf_trace<true>, dim3(trace_grid), dim3(256), c->trace_lds, c->stream, WP);
-        else
-          hipLaunchKernelGGL(rtd::wf_trace<false>, dim3(trace_grid), dim3(256), c->trace_lds, c->stream, WP);
+        launch_trace(c, count, dim3(trace_grid), WP);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(t1, c->stream));
         c->trace_events.push_back({t0, t1});

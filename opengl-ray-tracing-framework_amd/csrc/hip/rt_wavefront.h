@@ -166,9 +166,163 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
 }
 
 // ----------------------------------------------------------------------------- trace
-// Persistent traversal: every lane pulls queued rays one at a time (wave-aggregated atomics);
-// each loop iteration advances every busy lane by one internal node or one triangle.
-template <bool COUNT>
+// Persistent traversal: every lane pulls queued rays (one atomic per 64 rays per wave) and
+// runs the reference's near-first DFS (RT:338-390) with culling of subtrees that start beyond
+// the current closest hit.  Three wave schedules of the same per-lane steps (TraceMode):
+//   TM_IFIF  each iteration advances every busy lane by one internal node OR one triangle;
+//   TM_WW    while-while: internal nodes until every lane holds a leaf, then the leaf
+//            triangles, then the next pop (lanes doing the same kind of step stay together);
+//   TM_SPEC  while-while where a lane that reaches a leaf parks it and keeps descending until
+//            every lane has a parked leaf (Aila & Laine's speculative traversal).
+// All three visit a superset-free subset of the reference's nodes and return the same closest
+// hit (culling only drops subtrees whose entry distance exceeds the best hit so far).
+enum TraceMode { TM_IFIF = 0, TM_WW = 1, TM_SPEC = 2 };
+
+struct TraceLane {
+  f3 o, d, inv;
+  float best, bestt;
+  int besttri, sp, cur, tri_i, tri_end;
+  bool haveCur, anyhit;
+};
+
+// Exact-tie rule of the reference traversal (only the 4-wide schedule needs it: it visits
+// leaves in a different order).  The reference keeps the FIRST of equally distant hits in its
+// near-first DFS order (RT:328 / RT:356 use strict <).  Two triangles in one leaf: lower index
+// first.  Otherwise descend the binary tree to the node whose children separate the two
+// leaves (GNode.ref.z = DFS rank of the first right-subtree leaf): the reference enters the
+// left child first iff d1 < d2 (RT:373-382; both children were reached, so both d > 0).
+RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
+  const int ra = __float_as_int(P.trin[3 * a + 1].w), rb = __float_as_int(P.trin[3 * b + 1].w);
+  if (ra == rb) return a < b;
+  int node = P.root;
+  for (int guard = 0; guard < 64 && !ref_is_leaf(node); guard++) {
+    const GNode g = P.nodes[node];
+    const bool aL = ra < g.ref.z, bL = rb < g.ref.z;
+    if (aL == bL) {
+      node = aL ? g.ref.x : g.ref.y;
+      continue;
+    }
+    float e1, e2;
+    const float d1 = slab(L.o, L.inv, mk3(g.b0.x, g.b0.y, g.b0.z), mk3(g.b0.w, g.b1.x, g.b1.y), e1);
+    const float d2 = slab(L.o, L.inv, mk3(g.b1.z, g.b1.w, g.b2.x), mk3(g.b2.y, g.b2.z, g.b2.w), e2);
+    return aL == (d1 < d2);
+  }
+  return a < b;
+}
+
+// one triangle (RT:241-299, R1); true when it becomes the closest hit
+template <bool WIDE>
+RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
+  const float4 A = P.tri[3 * i], B = P.tri[3 * i + 1], Cc = P.tri[3 * i + 2];
+  const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+  const f3 ng = mk3(A.w, B.w, Cc.w);
+  const float dn = dot(ng, L.d);
+  if (fabs_(dn) < 0.00001f) return false;                           // RT:262
+  const float t = (dot(ng, p1) - dot(L.o, ng)) / dot(L.d, ng);       // RT:265
+  const float dist = t - 0.00001f;
+  if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
+  const f3 Pp = L.o + L.d * t;
+  const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
+  const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
+  const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
+  if (!((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0))) return false;
+  if (WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
+  L.best = dist;
+  L.besttri = i;
+  L.bestt = t;
+  return true;
+}
+
+// pop the next surviving subtree (RT:348); false when the stack is exhausted
+RTD bool tl_pop(TraceLane& L, const int2* slds, const int2* sovf, int stride, unsigned ovs, int KL,
+                bool cull) {
+  while (L.sp > 0) {
+    --L.sp;
+    const int2 ent = L.sp < KL ? slds[L.sp * stride] : sovf[(size_t)(L.sp - KL) * ovs];
+    if (cull && __int_as_float(ent.y) > cull_limit(L.best)) continue;
+    L.cur = ent.x;
+    return true;
+  }
+  return false;
+}
+
+// internal node L.cur (RT:361-385): both child boxes, near child first, far child stacked
+RTD void tl_node(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs,
+                 int KL, bool cull) {
+  const GNode nd = P.nodes[L.cur];
+  float e1, e2;
+  const float d1 = slab(L.o, L.inv, mk3(nd.b0.x, nd.b0.y, nd.b0.z), mk3(nd.b0.w, nd.b1.x, nd.b1.y), e1);
+  const float d2 = slab(L.o, L.inv, mk3(nd.b1.z, nd.b1.w, nd.b2.x), mk3(nd.b2.y, nd.b2.z, nd.b2.w), e2);
+  int nearRef = 0;
+  float nearE = 0.0f;
+  bool descend = false;
+  if (d1 > 0 && d2 > 0) {  // RT:373-382
+    const bool leftFirst = d1 < d2;
+    nearRef = leftFirst ? nd.ref.x : nd.ref.y;
+    nearE = leftFirst ? e1 : e2;
+    const int2 ent = make_int2(leftFirst ? nd.ref.y : nd.ref.x, __float_as_int(leftFirst ? e2 : e1));
+    if (L.sp < KL) slds[L.sp * stride] = ent;
+    else sovf[(size_t)(L.sp - KL) * ovs] = ent;
+    ++L.sp;
+    descend = true;
+  } else if (d1 > 0) {
+    nearRef = nd.ref.x; nearE = e1; descend = true;
+  } else if (d2 > 0) {
+    nearRef = nd.ref.y; nearE = e2; descend = true;
+  }
+  if (descend && cull && nearE > cull_limit(L.best)) descend = false;
+  L.cur = nearRef;
+  L.haveCur = descend || tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+}
+
+RTD void tl_push(TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs, int KL, int2 ent) {
+  if (L.sp < KL) slds[L.sp * stride] = ent;
+  else sovf[(size_t)(L.sp - KL) * ovs] = ent;
+  ++L.sp;
+}
+
+// 4-wide node L.cur: the four (grand)child boxes of the binary subtree it replaces, each with
+// the reference's slab test; survivors sorted by entry distance, nearest entered, rest stacked
+RTD void tl_qnode(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs,
+                  int KL, bool cull) {
+  const QNode* q = P.qnodes + L.cur;
+  const float4 lx = q->lox, ly = q->loy, lz = q->loz, hx = q->hix, hy = q->hiy, hz = q->hiz;
+  const int4 rf = q->ref;
+  const float lim = cull ? cull_limit(L.best) : __int_as_float(0x7f800000);
+  float k[4];
+  int r[4];
+  {
+    const float ax[4] = {lx.x, lx.y, lx.z, lx.w}, ay[4] = {ly.x, ly.y, ly.z, ly.w}, az[4] = {lz.x, lz.y, lz.z, lz.w};
+    const float bx[4] = {hx.x, hx.y, hx.z, hx.w}, by[4] = {hy.x, hy.y, hy.z, hy.w}, bz[4] = {hz.x, hz.y, hz.z, hz.w};
+    const int rr[4] = {rf.x, rf.y, rf.z, rf.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      float e;
+      const float dd = slab(L.o, L.inv, mk3(ax[c], ay[c], az[c]), mk3(bx[c], by[c], bz[c]), e);
+      const bool ok = dd > 0 && !(e > lim);
+      k[c] = ok ? e : __int_as_float(0x7f800000);
+      r[c] = ok ? rr[c] : Q_EMPTY;
+    }
+  }
+  // 5-comparator sorting network on (entry, ref)
+#define RT_CSWAP(a, b)                                      \
+  {                                                         \
+    const bool sw = k[b] < k[a];                            \
+    const float tk = sw ? k[b] : k[a];                      \
+    k[b] = sw ? k[a] : k[b]; k[a] = tk;                     \
+    const int tr = sw ? r[b] : r[a];                        \
+    r[b] = sw ? r[a] : r[b]; r[a] = tr;                     \
+  }
+  RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
+#undef RT_CSWAP
+  if (r[3] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[3], __float_as_int(k[3])));
+  if (r[2] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[2], __float_as_int(k[2])));
+  if (r[1] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[1], __float_as_int(k[1])));
+  L.cur = r[0];
+  L.haveCur = r[0] != Q_EMPTY || tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+}
+
+template <bool COUNT, int MODE, bool WIDE>
 __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
@@ -198,14 +352,18 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   const unsigned int ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
 
-  bool busy = false, anyhit = false, haveCur = false;
+  bool busy = false;
   // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
   unsigned int pool_next = 0, pool_end = 0;
   bool drained = false;
   const int lane = (int)(threadIdx.x & 63);
-  int entry = 0, sp = 0, cur = 0, tri_i = 0, tri_end = 0, besttri = -1;
-  float best = INF, bestt = 0.0f;
-  f3 o = splat(0.0f), d = splat(0.0f), inv = splat(0.0f);
+  int entry = 0, parked = 0;
+  bool haveParked = false;
+  TraceLane L;
+  L.o = L.d = L.inv = splat(0.0f);
+  L.best = INF; L.bestt = 0.0f; L.besttri = -1;
+  L.sp = L.cur = L.tri_i = L.tri_end = 0;
+  L.haveCur = L.anyhit = false;
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
 
   while (true) {
@@ -231,101 +389,99 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
           const unsigned int slot = pool_next + rank;
           entry = S.queue[qin][slot];
           const int path = entry >> 1;
-          anyhit = (entry & 1) != 0;
-          const float4 oo = anyhit ? S.so[path] : S.ro[path];
-          const float4 dd = anyhit ? S.sd[path] : S.rd[path];
-          o = mk3(oo.x, oo.y, oo.z);
-          d = mk3(dd.x, dd.y, dd.z);
-          inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-          best = INF;
-          besttri = -1;
-          bestt = 0.0f;
-          sp = 0;
-          cur = P.root;
-          haveCur = true;
-          tri_i = tri_end = 0;
+          L.anyhit = (entry & 1) != 0;
+          const float4 oo = L.anyhit ? S.so[path] : S.ro[path];
+          const float4 dd = L.anyhit ? S.sd[path] : S.rd[path];
+          L.o = mk3(oo.x, oo.y, oo.z);
+          L.d = mk3(dd.x, dd.y, dd.z);
+          L.inv = mk3(1.0f / L.d.x, 1.0f / L.d.y, 1.0f / L.d.z);
+          L.best = INF;
+          L.besttri = -1;
+          L.bestt = 0.0f;
+          L.sp = 0;
+          L.cur = WIDE ? P.qroot : P.root;
+          L.haveCur = true;
+          L.tri_i = L.tri_end = 0;
+          haveParked = false;
           busy = true;
         }
         pool_next += min((unsigned int)__popcll(idle), avail);
       }
     }
     if (!__any(busy)) break;
-    if (busy) {
-      bool finished = false;
-      if (tri_i < tri_end) {
-        // ---------------- one triangle of the current leaf (RT:241-299, R1)
-        const int i = tri_i++;
-        if (COUNT) v_tri++;
-        const float4 A = P.tri[3 * i], B = P.tri[3 * i + 1], Cc = P.tri[3 * i + 2];
-        const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
-        const f3 ng = mk3(A.w, B.w, Cc.w);
-        const float dn = dot(ng, d);
-        if (!(fabs_(dn) < 0.00001f)) {                              // RT:262
-          const float t = (dot(ng, p1) - dot(o, ng)) / dot(d, ng);  // RT:265
-          const float dist = t - 0.00001f;
-          if (t >= 0.0005f && dist < best) {                        // RT:268, RT:328/356
-            const f3 Pp = o + d * t;
-            const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
-            const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
-            const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
-            if ((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0)) {
-              best = dist;
-              besttri = i;
-              bestt = t;
-              if (anyhit) finished = true;
-            }
+    bool finished = false;
+    if (MODE == TM_IFIF) {
+      if (busy) {
+        if (L.tri_i < L.tri_end) {
+          if (COUNT) v_tri++;
+          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) finished = true;
+        } else if (L.haveCur) {
+          if (ref_is_leaf(L.cur)) {
+            if (COUNT) v_leaf++;
+            L.tri_i = leaf_first(L.cur);
+            L.tri_end = L.tri_i + leaf_count(L.cur);
+            L.haveCur = false;
+          } else {
+            if (COUNT) v_int++;
+            if (WIDE) tl_qnode(P, L, slds, sovf, stride, ovs, KL, cull);
+            else tl_node(P, L, slds, sovf, stride, ovs, KL, cull);
           }
         }
-      } else if (haveCur) {
-        if (ref_is_leaf(cur)) {
-          if (COUNT) v_leaf++;
-          tri_i = leaf_first(cur);
-          tri_end = tri_i + leaf_count(cur);
-          haveCur = false;
+        if (!finished && !L.haveCur && L.tri_i >= L.tri_end) {
+          L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+          if (!L.haveCur) finished = true;
+        }
+      }
+    } else {
+      // ---- internal nodes until every lane has a leaf (parked) or no work left
+      while (true) {
+        bool act;
+        if (MODE == TM_WW) {
+          act = busy && L.haveCur && !haveParked;
+          if (!__any(act)) break;
         } else {
-          if (COUNT) v_int++;
-          const GNode nd = P.nodes[cur];
-          float e1, e2;
-          const float d1 = slab(o, inv, mk3(nd.b0.x, nd.b0.y, nd.b0.z), mk3(nd.b0.w, nd.b1.x, nd.b1.y), e1);
-          const float d2 = slab(o, inv, mk3(nd.b1.z, nd.b1.w, nd.b2.x), mk3(nd.b2.y, nd.b2.z, nd.b2.w), e2);
-          int nearRef = 0;
-          float nearE = 0.0f;
-          bool descend = false;
-          if (d1 > 0 && d2 > 0) {  // RT:373-382: near first, far stacked
-            const bool leftFirst = d1 < d2;
-            nearRef = leftFirst ? nd.ref.x : nd.ref.y;
-            nearE = leftFirst ? e1 : e2;
-            const int2 ent = make_int2(leftFirst ? nd.ref.y : nd.ref.x, __float_as_int(leftFirst ? e2 : e1));
-            if (sp < KL) slds[sp * stride] = ent;
-            else sovf[(size_t)(sp - KL) * ovs] = ent;
-            ++sp;
-            descend = true;
-          } else if (d1 > 0) {
-            nearRef = nd.ref.x; nearE = e1; descend = true;
-          } else if (d2 > 0) {
-            nearRef = nd.ref.y; nearE = e2; descend = true;
+          if (__all(!busy || !L.haveCur || haveParked)) break;
+          act = busy && L.haveCur && !(haveParked && ref_is_leaf(L.cur));
+        }
+        if (COUNT) v_iter++;
+        if (act) {
+          if (ref_is_leaf(L.cur)) {
+            parked = L.cur;
+            haveParked = true;
+            if (MODE == TM_WW) L.haveCur = false;
+            else L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+          } else {
+            if (COUNT) v_int++;
+            if (WIDE) tl_qnode(P, L, slds, sovf, stride, ovs, KL, cull);
+            else tl_node(P, L, slds, sovf, stride, ovs, KL, cull);
           }
-          if (descend && cull && nearE > cull_limit(best)) descend = false;
-          cur = nearRef;
-          haveCur = descend;
         }
       }
-      if (!finished && !haveCur && tri_i >= tri_end) {
-        // pop the next surviving subtree (RT:348)
-        while (sp > 0) {
-          --sp;
-          const int2 ent = sp < KL ? slds[sp * stride] : sovf[(size_t)(sp - KL) * ovs];
-          if (cull && __int_as_float(ent.y) > cull_limit(best)) continue;
-          cur = ent.x;
-          haveCur = true;
-          break;
+      // ---- triangles of the parked leaf
+      if (haveParked) {
+        if (COUNT) v_leaf++;
+        L.tri_i = leaf_first(parked);
+        L.tri_end = L.tri_i + leaf_count(parked);
+        haveParked = false;
+      }
+      while (__any(L.tri_i < L.tri_end)) {
+        if (COUNT) v_iter++;
+        if (L.tri_i < L.tri_end) {
+          if (COUNT) v_tri++;
+          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+            finished = true;
+            L.tri_end = L.tri_i;
+          }
         }
-        if (!haveCur) finished = true;
       }
-      if (finished) {
-        S.res[entry] = make_int2(besttri, __float_as_int(bestt));
-        busy = false;
+      if (busy && !finished && !L.haveCur) {
+        L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+        if (!L.haveCur) finished = true;
       }
+    }
+    if (busy && finished) {
+      S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
+      busy = false;
     }
   }
   if (COUNT) {

@@ -65,3 +65,33 @@ def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_m
     img3, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
     assert bit_mismatch(img1, ref)[0] == 0.0
     assert bit_mismatch(img3, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("width", ["4", "2"], ids=["bvh4", "bvh2"])
+def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monkeypatch, width):
+    """Two copies of the bunny at the same place with different materials: every hit on it is an
+    exact distance tie between two triangles in different leaves.  The reference keeps the one
+    its near-first DFS reaches first; the 4-wide traversal visits leaves in another order and
+    must resolve each tie to that same triangle (tie_wins), the binary one by construction."""
+    twin = cf.Obj("bunny_4000", "golden", (0, 0, 0), (2.2, -2.5, 3), (2, 2, 2), False)
+    sd = cf.build_scene((cf.FLOOR, cf.BUNNY, twin))
+    W, H = 64, 36
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 1)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    monkeypatch.setenv("RT_BVH_WIDTH", width)
+    img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert st["rays"] == cnt["rays"]
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_binary_wavefront_traversal_matches(gpu_renderer, env_maps, monkeypatch):
+    """RT_BVH_WIDTH=2 keeps the wavefront trace on the binary tree (reference visit order)."""
+    sd = cf.config_scene("C3")
+    W, H = 64, 36
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    monkeypatch.setenv("RT_BVH_WIDTH", "2")
+    img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert bit_mismatch(img, ref)[0] == 0.0

@@ -18,14 +18,14 @@ tag = sys.argv[2]
 cfg = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}
 dst = Path(__file__).resolve().parent.parent / "profiles"
 dst.mkdir(exist_ok=True)
-KERNEL = "rt_path_kernel<false>"
+KERNEL = "wf_trace<false"   # the timed bench launches (the visit-counting frame uses wf_trace<true)
 
 shutil.copyfile(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
 durs = []
 for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")):
     if KERNEL in r["Kernel_Name"]:
         durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-        vgpr, lds = r["VGPR_Count"], r["LDS_Block_Size"]
+        vgpr, lds = r.get("Arch_VGPR_Count", r.get("VGPR_Count", 0)), r["LDS_Block_Size"]
 
 
 def counters(name):
@@ -38,7 +38,7 @@ def counters(name):
 
 pf, pw, sq = counters("pmc_fetch"), counters("pmc_write"), counters("pmc_sq")
 summary = {
-    "kernel": KERNEL,
+    "kernel": "wf_trace",
     "launches_traced": len(durs),
     "avg_launch_ms": round(statistics.mean(durs), 4),
     "min_launch_ms": round(min(durs), 4),
@@ -51,4 +51,6 @@ summary = {
 }
 summary.update(cfg)
 (dst / f"{tag}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
+if cfg.get("config"):
+    (dst / f"pmc_traffic_{cfg['config']}.json").write_text(json.dumps(summary, indent=1) + "\n")
 print(json.dumps(summary, indent=1))
