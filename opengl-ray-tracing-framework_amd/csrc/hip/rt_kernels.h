@@ -42,6 +42,7 @@ struct KParams {
   const QNode* __restrict__ qnodes;  // 4-wide collapse of `nodes` (wavefront trace, TW_WIDE)
   int qroot;
   int lds_entries;                  // wavefront traversal: stack entries kept in LDS
+  int pool_chunk;                   // wavefront traversal: rays claimed per queue atomic
   int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]
   unsigned int ovf_lanes;
   const float4* __restrict__ tri;   // 3 per triangle: {p1, Ng.x} {p2, Ng.y} {p3, Ng.z}

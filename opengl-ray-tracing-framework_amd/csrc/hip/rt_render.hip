@@ -63,6 +63,7 @@ struct rt_ctx {
   int trace_bpc = 0;                          // wavefront traversal kernel
   int trace_lds_entries = 0, trace_lds = 0;
   int trace_mode = 0;                         // rtd::TraceMode
+  int pool_chunk = 256;                       // rays per queue atomic in wf_trace
   int2* d_stack_ovf = nullptr;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
@@ -235,6 +236,17 @@ int occupancy(rt_ctx* c) {
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256,
                                                          c->trace_lds));
   c->trace_bpc = std::max(1, bpc);
+  if (const char* e = getenv("RT_TRACE_BPC")) c->trace_bpc = std::max(1, atoi(e));
+  if (const char* e = getenv("RT_POOL_CHUNK")) c->pool_chunk = std::max(64, atoi(e) / 64 * 64);
+  if (getenv("RT_DEBUG")) {
+    fprintf(stderr, "[rt] trace: lds entries %d (%d B/block), occupancy API %d blocks/CU, using %d; megakernel %d\n",
+            kl, c->trace_lds, bpc, c->trace_bpc, c->blocks_per_cu);
+    for (int l = 0; l <= 40960; l += 8192) {
+      int b = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256, l);
+      fprintf(stderr, "[rt]   occupancy(lds=%d) = %d\n", l, b);
+    }
+  }
   const size_t lanes = (size_t)c->n_cus * c->trace_bpc * 256;
   const int entries = std::max(c->stack_entries, c->qstack_entries);
   const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2);
@@ -711,6 +723,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const unsigned int shade_grid = gen_grid;
       const unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
       WP.K.lds_entries = c->trace_lds_entries;
+      WP.K.pool_chunk = c->pool_chunk;
       WP.K.stack_ovf = c->d_stack_ovf;
       WP.K.ovf_lanes = trace_grid * 256u;
       HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));

@@ -185,6 +185,26 @@ struct TraceLane {
   bool haveCur, anyhit;
 };
 
+// Traversal stack of one lane: entries [0, KL) in LDS at lds[j * TL_LANES] ([entry][lane], the
+// block is always 256 lanes, so addresses are shifts), deeper ones in the global overflow
+// column (explicitly global, so the accesses never become FLAT and never wait on LDS counters).
+typedef __attribute__((address_space(1))) unsigned long long gu64;  // {ref, key} packed
+RTD unsigned long long pack_ent(int2 e) { return (unsigned long long)(uint32_t)e.x | ((unsigned long long)(uint32_t)e.y << 32); }
+RTD int2 unpack_ent(unsigned long long v) { return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32)); }
+constexpr int TL_LANES = 256;
+struct TraceStack {
+  int2* lds;
+  gu64* ovf;
+  unsigned ovs;
+  int KL;
+};
+
+// byte-offset loads from a uniform base: the compiler emits the saddr form (32-bit lane offset)
+template <class T>
+RTD T ld(const void* base, uint32_t byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 // Exact-tie rule of the reference traversal (only the 4-wide schedule needs it: it visits
 // leaves in a different order).  The reference keeps the FIRST of equally distant hits in its
 // near-first DFS order (RT:328 / RT:356 use strict <).  Two triangles in one leaf: lower index
@@ -196,7 +216,7 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
   if (ra == rb) return a < b;
   int node = P.root;
   for (int guard = 0; guard < 64 && !ref_is_leaf(node); guard++) {
-    const GNode g = P.nodes[node];
+    const GNode g = ld<GNode>(P.nodes, (uint32_t)node * 64u);
     const bool aL = ra < g.ref.z, bL = rb < g.ref.z;
     if (aL == bL) {
       node = aL ? g.ref.x : g.ref.y;
@@ -213,12 +233,19 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
 // one triangle (RT:241-299, R1); true when it becomes the closest hit
 template <bool WIDE>
 RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
-  const float4 A = P.tri[3 * i], B = P.tri[3 * i + 1], Cc = P.tri[3 * i + 2];
+  const uint32_t off = (uint32_t)i * 48u;
+  const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d);
   if (fabs_(dn) < 0.00001f) return false;                           // RT:262
-  const float t = (dot(ng, p1) - dot(L.o, ng)) / dot(L.d, ng);       // RT:265
+  const float num = dot(ng, p1) - dot(L.o, ng);
+  // Conservative early reject before the correctly rounded division: num * rcp(dn) is within
+  // ~2^-21 of num / dn (|dn| >= 1e-5, no denormals), so outside these margins the exact t
+  // fails RT:268 or the closest-hit test for certain.  NaN never rejects.
+  const float qa = num * __builtin_amdgcn_rcpf(dn);
+  if (qa < 0.0005f * (1.0f - 0x1p-16f) || qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
+  const float t = num / dot(L.d, ng);                                // RT:265
   const float dist = t - 0.00001f;
   if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
   const f3 Pp = L.o + L.d * t;
@@ -233,13 +260,19 @@ RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   return true;
 }
 
+RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
+  if (L.sp < S.KL) S.lds[L.sp * TL_LANES] = ent;
+  else S.ovf[(size_t)(L.sp - S.KL) * S.ovs] = pack_ent(ent);
+  ++L.sp;
+}
+
 // pop the next surviving subtree (RT:348); false when the stack is exhausted
-RTD bool tl_pop(TraceLane& L, const int2* slds, const int2* sovf, int stride, unsigned ovs, int KL,
-                bool cull) {
+RTD bool tl_pop(TraceLane& L, const TraceStack& S, bool cull) {
+  const float lim = cull_limit(L.best);
   while (L.sp > 0) {
     --L.sp;
-    const int2 ent = L.sp < KL ? slds[L.sp * stride] : sovf[(size_t)(L.sp - KL) * ovs];
-    if (cull && __int_as_float(ent.y) > cull_limit(L.best)) continue;
+    const int2 ent = L.sp < S.KL ? S.lds[L.sp * TL_LANES] : unpack_ent(S.ovf[(size_t)(L.sp - S.KL) * S.ovs]);
+    if (cull && __int_as_float(ent.y) > lim) continue;
     L.cur = ent.x;
     return true;
   }
@@ -247,47 +280,40 @@ RTD bool tl_pop(TraceLane& L, const int2* slds, const int2* sovf, int stride, un
 }
 
 // internal node L.cur (RT:361-385): both child boxes, near child first, far child stacked
-RTD void tl_node(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs,
-                 int KL, bool cull) {
-  const GNode nd = P.nodes[L.cur];
+RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+  const uint32_t off = (uint32_t)L.cur * 64u;
+  const float4 b0 = ld<float4>(P.nodes, off), b1 = ld<float4>(P.nodes, off + 16u), b2 = ld<float4>(P.nodes, off + 32u);
+  const int2 ref = ld<int2>(P.nodes, off + 48u);
   float e1, e2;
-  const float d1 = slab(L.o, L.inv, mk3(nd.b0.x, nd.b0.y, nd.b0.z), mk3(nd.b0.w, nd.b1.x, nd.b1.y), e1);
-  const float d2 = slab(L.o, L.inv, mk3(nd.b1.z, nd.b1.w, nd.b2.x), mk3(nd.b2.y, nd.b2.z, nd.b2.w), e2);
+  const float d1 = slab(L.o, L.inv, mk3(b0.x, b0.y, b0.z), mk3(b0.w, b1.x, b1.y), e1);
+  const float d2 = slab(L.o, L.inv, mk3(b1.z, b1.w, b2.x), mk3(b2.y, b2.z, b2.w), e2);
   int nearRef = 0;
   float nearE = 0.0f;
   bool descend = false;
   if (d1 > 0 && d2 > 0) {  // RT:373-382
     const bool leftFirst = d1 < d2;
-    nearRef = leftFirst ? nd.ref.x : nd.ref.y;
+    nearRef = leftFirst ? ref.x : ref.y;
     nearE = leftFirst ? e1 : e2;
-    const int2 ent = make_int2(leftFirst ? nd.ref.y : nd.ref.x, __float_as_int(leftFirst ? e2 : e1));
-    if (L.sp < KL) slds[L.sp * stride] = ent;
-    else sovf[(size_t)(L.sp - KL) * ovs] = ent;
-    ++L.sp;
+    tl_push(L, S, make_int2(leftFirst ? ref.y : ref.x, __float_as_int(leftFirst ? e2 : e1)));
     descend = true;
   } else if (d1 > 0) {
-    nearRef = nd.ref.x; nearE = e1; descend = true;
+    nearRef = ref.x; nearE = e1; descend = true;
   } else if (d2 > 0) {
-    nearRef = nd.ref.y; nearE = e2; descend = true;
+    nearRef = ref.y; nearE = e2; descend = true;
   }
   if (descend && cull && nearE > cull_limit(L.best)) descend = false;
   L.cur = nearRef;
-  L.haveCur = descend || tl_pop(L, slds, sovf, stride, ovs, KL, cull);
-}
-
-RTD void tl_push(TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs, int KL, int2 ent) {
-  if (L.sp < KL) slds[L.sp * stride] = ent;
-  else sovf[(size_t)(L.sp - KL) * ovs] = ent;
-  ++L.sp;
+  L.haveCur = descend || tl_pop(L, S, cull);
 }
 
 // 4-wide node L.cur: the four (grand)child boxes of the binary subtree it replaces, each with
 // the reference's slab test; survivors sorted by entry distance, nearest entered, rest stacked
-RTD void tl_qnode(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int stride, unsigned ovs,
-                  int KL, bool cull) {
-  const QNode* q = P.qnodes + L.cur;
-  const float4 lx = q->lox, ly = q->loy, lz = q->loz, hx = q->hix, hy = q->hiy, hz = q->hiz;
-  const int4 rf = q->ref;
+RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+  const uint32_t off = (uint32_t)L.cur << 7;
+  const float4 lx = ld<float4>(P.qnodes, off), ly = ld<float4>(P.qnodes, off + 16u),
+               lz = ld<float4>(P.qnodes, off + 32u), hx = ld<float4>(P.qnodes, off + 48u),
+               hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
+  const int4 rf = ld<int4>(P.qnodes, off + 96u);
   const float lim = cull ? cull_limit(L.best) : __int_as_float(0x7f800000);
   float k[4];
   int r[4];
@@ -304,7 +330,8 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int st
       r[c] = ok ? rr[c] : Q_EMPTY;
     }
   }
-  // 5-comparator sorting network on (entry, ref)
+  const int n = (r[0] != Q_EMPTY) + (r[1] != Q_EMPTY) + (r[2] != Q_EMPTY) + (r[3] != Q_EMPTY);
+  // 5-comparator sorting network on (entry, ref); empty slots (key +inf) sink to the end
 #define RT_CSWAP(a, b)                                      \
   {                                                         \
     const bool sw = k[b] < k[a];                            \
@@ -315,11 +342,24 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, int2* slds, int2* sovf, int st
   }
   RT_CSWAP(0, 1) RT_CSWAP(2, 3) RT_CSWAP(0, 2) RT_CSWAP(1, 3) RT_CSWAP(1, 2)
 #undef RT_CSWAP
-  if (r[3] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[3], __float_as_int(k[3])));
-  if (r[2] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[2], __float_as_int(k[2])));
-  if (r[1] != Q_EMPTY) tl_push(L, slds, sovf, stride, ovs, KL, make_int2(r[1], __float_as_int(k[1])));
+  // a +inf key can only be a valid child in degenerate cases; keep the entry count exact
+  const int2 e1 = make_int2(r[1], __float_as_int(k[1])), e2 = make_int2(r[2], __float_as_int(k[2])),
+             e3 = make_int2(r[3], __float_as_int(k[3]));
+  if (L.sp + 3 <= S.KL && r[0] != Q_EMPTY && (n < 2 || r[n - 1] != Q_EMPTY)) {
+    // branch-free: the far-to-near entries 3, 2, 1 land at sp, sp+[n>=4], sp+[n>=4]+[n>=3];
+    // an empty entry is overwritten by the next write, so exactly n-1 entries survive
+    const int a0 = L.sp, a1 = a0 + (n >= 4), a2 = a1 + (n >= 3);
+    S.lds[a0 * TL_LANES] = e3;
+    S.lds[a1 * TL_LANES] = e2;
+    S.lds[a2 * TL_LANES] = e1;
+    L.sp += n - 1;
+  } else {
+    if (r[3] != Q_EMPTY) tl_push(L, S, e3);
+    if (r[2] != Q_EMPTY) tl_push(L, S, e2);
+    if (r[1] != Q_EMPTY) tl_push(L, S, e1);
+  }
   L.cur = r[0];
-  L.haveCur = r[0] != Q_EMPTY || tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+  L.haveCur = r[0] != Q_EMPTY || tl_pop(L, S, cull);
 }
 
 template <bool COUNT, int MODE, bool WIDE>
@@ -342,19 +382,20 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
     }
     return;
   }
-  const int stride = blockDim.x;
   // traversal stack: the top lds_entries entries of every lane in LDS ([entry][lane], 8-B
   // {ref, entry distance} pairs, conflict-free ds_read/write_b64), deeper entries in a global
   // overflow region ([entry][grid lane], coalesced) that only very deep stacks touch.
-  const int KL = P.lds_entries;
-  int2* slds = reinterpret_cast<int2*>(smem) + threadIdx.x;
-  int2* sovf = P.stack_ovf + (blockIdx.x * blockDim.x + threadIdx.x);
-  const unsigned int ovs = P.ovf_lanes;
+  TraceStack TS;
+  TS.KL = P.lds_entries;
+  TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
+  TS.ovf = (gu64*)(P.stack_ovf) + (blockIdx.x * TL_LANES + threadIdx.x);
+  TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
 
   bool busy = false;
   // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
   unsigned int pool_next = 0, pool_end = 0;
+  const unsigned int tail_rays = gridDim.x * TL_LANES * 4u;
   bool drained = false;
   const int lane = (int)(threadIdx.x & 63);
   int entry = 0, parked = 0;
@@ -368,18 +409,22 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
 
   while (true) {
     if (COUNT) v_iter++;
-    // ---- refill idle lanes from the wave's pool; one global atomic per 64 rays
+    // ---- refill idle lanes from the wave's pool.  One counter serves the whole chip and a
+    // single atomic address sustains only ~90 atomics/us, so the pool is claimed in big chunks
+    // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
+    // queue so the last rays still spread over all waves.
     const unsigned long long idle = __ballot(!busy);
     if (idle && !drained) {
       if (pool_next >= pool_end) {
+        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : 64u;
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&S.cnt[4], 64u);
+        if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= nq) {
           drained = true;
         } else {
           pool_next = base;
-          pool_end = min(base + 64u, nq);
+          pool_end = min(base + chunk, nq);
         }
       }
       if (!drained || pool_next < pool_end) {
@@ -423,12 +468,12 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
             L.haveCur = false;
           } else {
             if (COUNT) v_int++;
-            if (WIDE) tl_qnode(P, L, slds, sovf, stride, ovs, KL, cull);
-            else tl_node(P, L, slds, sovf, stride, ovs, KL, cull);
+            if (WIDE) tl_qnode(P, L, TS, cull);
+            else tl_node(P, L, TS, cull);
           }
         }
         if (!finished && !L.haveCur && L.tri_i >= L.tri_end) {
-          L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+          L.haveCur = tl_pop(L, TS, cull);
           if (!L.haveCur) finished = true;
         }
       }
@@ -449,11 +494,11 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
             parked = L.cur;
             haveParked = true;
             if (MODE == TM_WW) L.haveCur = false;
-            else L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+            else L.haveCur = tl_pop(L, TS, cull);
           } else {
             if (COUNT) v_int++;
-            if (WIDE) tl_qnode(P, L, slds, sovf, stride, ovs, KL, cull);
-            else tl_node(P, L, slds, sovf, stride, ovs, KL, cull);
+            if (WIDE) tl_qnode(P, L, TS, cull);
+            else tl_node(P, L, TS, cull);
           }
         }
       }
@@ -475,7 +520,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
         }
       }
       if (busy && !finished && !L.haveCur) {
-        L.haveCur = tl_pop(L, slds, sovf, stride, ovs, KL, cull);
+        L.haveCur = tl_pop(L, TS, cull);
         if (!L.haveCur) finished = true;
       }
     }
