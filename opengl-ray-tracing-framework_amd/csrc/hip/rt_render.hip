@@ -68,8 +68,15 @@ struct rt_ctx {
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
   void* wf_mem = nullptr;
-  size_t wf_paths = 0;
-  rtd::WFState wf{};
+  size_t wf_paths = 0;                        // path slots per frame group
+  rtd::WFState wf{};                          // pixel lists (shared by every group)
+  // Frame groups: the frames of one batch are split into n_groups independent wavefronts with
+  // their own path state, run on their own streams, so the latency tail of one group's late
+  // bounces overlaps the other's busy passes; blends stay in frame order (events).
+  static constexpr int MAX_GROUPS = 4;
+  int n_groups = 2;
+  rtd::WFState wfg[MAX_GROUPS]{};
+  hipStream_t aux[MAX_GROUPS] = {};
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
@@ -249,7 +256,7 @@ int occupancy(rt_ctx* c) {
   }
   const size_t lanes = (size_t)c->n_cus * c->trace_bpc * 256;
   const int entries = std::max(c->stack_entries, c->qstack_entries);
-  const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2);
+  const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2) * c->n_groups;
   if (need > c->stack_ovf_bytes) {
     dfree(c->d_stack_ovf);
     HIPCHK(c, hipMalloc(&c->d_stack_ovf, need));
@@ -259,28 +266,28 @@ int occupancy(rt_ctx* c) {
 }
 
 template <bool COUNT, bool WIDE>
-void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP) {
+void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
   switch (c->trace_mode) {
     case rtd::TM_IFIF:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_IFIF, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_IFIF, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
       break;
     case rtd::TM_WW:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_WW, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_WW, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
       break;
     default:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_SPEC, WIDE>), grid, dim3(256), c->trace_lds, c->stream, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_SPEC, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
   }
 }
 
 template <bool COUNT>
-void launch_trace_t(rt_ctx* c, dim3 grid, const rtd::WFParams& WP) {
-  if (c->wide) launch_trace_w<COUNT, true>(c, grid, WP);
-  else launch_trace_w<COUNT, false>(c, grid, WP);
+void launch_trace_t(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
+  if (c->wide) launch_trace_w<COUNT, true>(c, grid, WP, st);
+  else launch_trace_w<COUNT, false>(c, grid, WP, st);
 }
 
-void launch_trace(rt_ctx* c, bool count, dim3 grid, const rtd::WFParams& WP) {
-  if (count) launch_trace_t<true>(c, grid, WP);
-  else launch_trace_t<false>(c, grid, WP);
+void launch_trace(rt_ctx* c, bool count, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
+  if (count) launch_trace_t<true>(c, grid, WP, st);
+  else launch_trace_t<false>(c, grid, WP, st);
 }
 
 hipEvent_t take_event(rt_ctx* c) {
@@ -295,27 +302,32 @@ hipEvent_t take_event(rt_ctx* c) {
 }
 
 // Path-state buffers of the wavefront path, carved from one allocation.
+// Path-state buffers of the wavefront path: `paths` slots for each of the n_groups frame
+// groups, carved from one allocation (216 B per slot + counters).
 int alloc_wavefront(rt_ctx* c, size_t paths) {
   if (c->wf_mem && c->wf_paths >= paths) return RT_OK;
-  if (c->wf_mem) {  // grow: earlier launches on the stream may still read the old state
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->wf_mem) {  // grow: earlier launches on the streams may still read the old state
+    HIPCHK(c, hipDeviceSynchronize());
     (void)hipFree(c->wf_mem);
     c->wf_mem = nullptr;
   }
   const size_t P = std::max<size_t>(paths, 64);
-  const size_t bytes = P * (6 * 16 + 4 * 16 + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
-  HIPCHK(c, hipMalloc(&c->wf_mem, bytes));
+  const size_t per = P * (6 * 16 + 4 * 16 + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
+  HIPCHK(c, hipMalloc(&c->wf_mem, per * c->n_groups));
   char* p = static_cast<char*>(c->wf_mem);
   auto carve = [&](size_t n) { char* q = p; p += (n + 255) & ~size_t(255); return q; };
-  c->wf.s0 = (float4*)carve(P * 16); c->wf.s1 = (float4*)carve(P * 16); c->wf.s2 = (float4*)carve(P * 16);
-  c->wf.s3 = (float4*)carve(P * 16); c->wf.s4 = (float4*)carve(P * 16); c->wf.s5 = (uint4*)carve(P * 16);
-  c->wf.ro = (float4*)carve(P * 16); c->wf.rd = (float4*)carve(P * 16);
-  c->wf.so = (float4*)carve(P * 16); c->wf.sd = (float4*)carve(P * 16);
-  c->wf.res = (int2*)carve(P * 16);
-  c->wf.fin = (float4*)carve(P * 16);
-  c->wf.queue[0] = (int*)carve(P * 8); c->wf.queue[1] = (int*)carve(P * 8);
-  c->wf.active[0] = (int*)carve(P * 4); c->wf.active[1] = (int*)carve(P * 4);
-  c->wf.cnt = (unsigned int*)carve(64);
+  for (int g = 0; g < c->n_groups; g++) {
+    rtd::WFState& w = c->wfg[g];
+    w.s0 = (float4*)carve(P * 16); w.s1 = (float4*)carve(P * 16); w.s2 = (float4*)carve(P * 16);
+    w.s3 = (float4*)carve(P * 16); w.s4 = (float4*)carve(P * 16); w.s5 = (uint4*)carve(P * 16);
+    w.ro = (float4*)carve(P * 16); w.rd = (float4*)carve(P * 16);
+    w.so = (float4*)carve(P * 16); w.sd = (float4*)carve(P * 16);
+    w.res = (int2*)carve(P * 16);
+    w.fin = (float4*)carve(P * 16);
+    w.queue[0] = (int*)carve(P * 8); w.queue[1] = (int*)carve(P * 8);
+    w.active[0] = (int*)carve(P * 4); w.active[1] = (int*)carve(P * 4);
+    w.cnt = (unsigned int*)carve(64);
+  }
   c->wf_paths = P;
   return RT_OK;
 }
@@ -339,6 +351,7 @@ int rt_create(int hip_device, rt_ctx** out) {
   c->n_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
   c->own_stream = true;
+  if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
@@ -358,6 +371,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
+  for (auto& a : c->aux) if (a) (void)hipStreamDestroy(a);
   dfree(c->d_pix);
   dfree(c->d_stack_ovf);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -663,8 +677,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   HIPCHK(c, hipSetDevice(c->device));
   if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
     const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
-    const int rc = alloc_wavefront(c, (size_t)std::min(c->frames_cap, (int)n_frames) * nv);
+    const int per_group = (std::min(c->frames_cap, (int)n_frames) + c->n_groups - 1) / c->n_groups;
+    const int rc = alloc_wavefront(c, (size_t)per_group * nv);
     if (rc) return rc;
+    for (int g = 1; g < c->n_groups; g++)
+      if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
   }
   int done = 0;
   while (done < n_frames) {
@@ -713,39 +730,99 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       HIPCHK(c, hipGetLastError());
       c->trace_launches++;
     } else {
-      rtd::WFParams WP;
-      WP.K = P;
-      WP.K.n_work = (unsigned)c->n_valid;
-      WP.S = c->wf;
-      WP.n_frames = nf;
-      const unsigned int slots = (unsigned)nf * (unsigned)c->n_valid;
-      const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots + 255) / 256));
-      const unsigned int shade_grid = gen_grid;
+      // split the batch into frame groups (frames [f0, f1) each), one stream per group
+      const int G = std::min(c->n_groups, nf);
+      static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
       const unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
-      WP.K.lds_entries = c->trace_lds_entries;
-      WP.K.pool_chunk = c->pool_chunk;
-      WP.K.stack_ovf = c->d_stack_ovf;
-      WP.K.ovf_lanes = trace_grid * 256u;
-      HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));
-      WP.pass = 0;
-      hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, c->stream, WP);
-      HIPCHK(c, hipGetLastError());
-      for (int pass = 0; pass <= std::max(0, fp->max_bounce); pass++) {
-        WP.pass = pass;
-        hipEvent_t t0 = take_event(c), t1 = take_event(c);
-        if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
-        HIPCHK(c, hipEventRecord(t0, c->stream));
-        launch_trace(c, count, dim3(trace_grid), WP);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipEventRecord(t1, c->stream));
-        c->trace_events.push_back({t0, t1});
-        c->trace_launches++;
-        hipLaunchKernelGGL(rtd::wf_shade, dim3(shade_grid), dim3(256), 0, c->stream, WP);
+      const size_t ovf_group = c->stack_ovf_bytes / sizeof(int2) / (size_t)c->n_groups;
+      rtd::WFParams WG[rt_ctx::MAX_GROUPS];
+      hipStream_t sg[rt_ctx::MAX_GROUPS];
+      unsigned int slots_g[rt_ctx::MAX_GROUPS];
+      for (int g = 0; g < G; g++) {
+        const int f0 = g * nf / G, f1 = (g + 1) * nf / G;
+        rtd::WFParams& WP = WG[g];
+        WP.K = P;
+        for (int f = f0; f < f1; f++) {
+          WP.K.loop_num[f - f0] = P.loop_num[f];
+          WP.K.rand_origin[f - f0] = P.rand_origin[f];
+        }
+        WP.K.n_frames = f1 - f0;
+        WP.K.n_work = (unsigned)c->n_valid;
+        WP.K.lds_entries = c->trace_lds_entries;
+        WP.K.pool_chunk = c->pool_chunk;
+        WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)g * ovf_group : nullptr;
+        WP.K.ovf_lanes = trace_grid * 256u;
+        WP.S = c->wfg[g];
+        WP.S.pix_xy = c->wf.pix_xy;
+        WP.S.pix_acc = c->wf.pix_acc;
+        WP.n_frames = f1 - f0;
+        WP.pass = 0;
+        slots_g[g] = (unsigned)(f1 - f0) * (unsigned)c->n_valid;
+        sg[g] = g == 0 ? c->stream : c->aux[g];
+      }
+      // aux streams start after everything already queued on the caller's stream
+      if (G > 1) {
+        hipEvent_t es = take_event(c);
+        if (!es) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+        HIPCHK(c, hipEventRecord(es, c->stream));
+        for (int g = 1; g < G; g++) HIPCHK(c, hipStreamWaitEvent(sg[g], es, 0));
+        c->event_pool.push_back(es);  // reusable once the waits are enqueued
+      }
+      for (int g = 0; g < G; g++) {
+        const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots_g[g] + 255) / 256));
+        HIPCHK(c, hipMemsetAsync(WG[g].S.cnt, 0, 64, sg[g]));
+        hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, sg[g], WG[g]);
         HIPCHK(c, hipGetLastError());
       }
+      for (int pass = 0; pass <= std::max(0, fp->max_bounce); pass++) {
+        for (int g = 0; g < G; g++) {  // interleaved issue: every stream always has queued work
+          rtd::WFParams& WP = WG[g];
+          WP.pass = pass;
+          hipEvent_t t0 = take_event(c), t1 = take_event(c);
+          if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+          HIPCHK(c, hipEventRecord(t0, sg[g]));
+          launch_trace(c, count, dim3(trace_grid), WP, sg[g]);
+          HIPCHK(c, hipGetLastError());
+          HIPCHK(c, hipEventRecord(t1, sg[g]));
+          c->trace_events.push_back({t0, t1});
+          c->trace_launches++;
+          if (debug_passes) {  // development aid: per-pass rays / visits / duration (syncs!)
+            unsigned long long h[8];
+            unsigned int q[2];
+            HIPCHK(c, hipStreamSynchronize(sg[g]));
+            float ms = 0.0f;
+            HIPCHK(c, hipEventElapsedTime(&ms, t0, t1));
+            HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu max %llu\n",
+                    g, pass, q[0], ms, h[2], h[3], h[4], h[5], h[6]);
+          }
+          const unsigned int shade_grid = std::max(
+              1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
+          hipLaunchKernelGGL(rtd::wf_shade, dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          HIPCHK(c, hipGetLastError());
+        }
+      }
+      // progressive blends in frame order: group g after group g-1
       const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
-      hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, c->stream, WP);
-      HIPCHK(c, hipGetLastError());
+      for (int g = 0; g < G; g++) {
+        if (g > 0) {
+          hipEvent_t eb = take_event(c);
+          if (!eb) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+          HIPCHK(c, hipEventRecord(eb, sg[g - 1]));
+          HIPCHK(c, hipStreamWaitEvent(sg[g], eb, 0));
+          c->event_pool.push_back(eb);
+        }
+        hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WG[g]);
+        HIPCHK(c, hipGetLastError());
+      }
+      if (G > 1) {  // the caller's stream joins the last group
+        hipEvent_t ej = take_event(c);
+        if (!ej) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+        HIPCHK(c, hipEventRecord(ej, sg[G - 1]));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, ej, 0));
+        c->event_pool.push_back(ej);
+      }
     }
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->events.push_back({e0, e1});

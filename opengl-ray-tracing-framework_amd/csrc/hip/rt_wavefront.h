@@ -94,28 +94,17 @@ RTD unsigned int wave_append(unsigned int* counter, bool want) {
   return base;
 }
 
-// Block-aggregated append: every thread of the block calls it (block-uniform control flow);
-// a thread appends `n` (0, 1 or 2) entries.  One global atomic per block (a single counter
-// word saturates near 88 atomics/us on MI355X, so per-wave or per-lane appends would
-// serialise a 2M-path pass).  Returns the thread's first slot.
-RTD unsigned int block_append(unsigned int* counter, unsigned int n, unsigned int* smem4 /* >= 5 uints */) {
-  const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+// Wave-aggregated append into a block-local LDS list: every lane of the wave calls it
+// (wave-uniform control flow) with n = 0, 1 or 2 entries; one LDS atomic per wave.
+RTD unsigned int wave_lds_append(unsigned int* lcount, unsigned int n) {
+  const int lane = (int)(threadIdx.x & 63);
   const unsigned long long b1 = __ballot(n >= 1u), b2 = __ballot(n >= 2u);
   const unsigned long long below = (1ull << lane) - 1ull;
   const unsigned int mine = (unsigned int)(__popcll(b1 & below) + __popcll(b2 & below));
   const unsigned int wtot = (unsigned int)(__popcll(b1) + __popcll(b2));
-  if (lane == 0) smem4[wave] = wtot;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned int acc = 0;
-    const int nw = (int)(blockDim.x >> 6);
-    for (int k = 0; k < nw; k++) { unsigned int t = smem4[k]; smem4[k] = acc; acc += t; }
-    smem4[4] = acc ? atomicAdd(counter, acc) : 0u;
-  }
-  __syncthreads();
-  const unsigned int slot = smem4[4] + smem4[wave] + mine;
-  __syncthreads();  // smem4 reused by the next call
-  return slot;
+  unsigned int base = 0;
+  if (lane == 0 && wtot) base = atomicAdd(lcount, wtot);
+  return (unsigned int)__shfl((int)base, 0) + mine;
 }
 
 // ------------------------------------------------------------------------------- gen
@@ -179,11 +168,18 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
 enum TraceMode { TM_IFIF = 0, TM_WW = 1, TM_SPEC = 2 };
 
 struct TraceLane {
-  f3 o, d, inv;
+  // ray as scalars (f3 members made SROA keep the lane in scratch memory)
+  float ox, oy, oz, dx, dy, dz, ix, iy, iz;
+  RTD f3 o() const { return mk3(ox, oy, oz); }
+  RTD f3 d() const { return mk3(dx, dy, dz); }
+  RTD f3 inv() const { return mk3(ix, iy, iz); }
   float best, bestt;
   int besttri, sp, cur, tri_i, tri_end;
-  bool haveCur, anyhit;
+  int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
+  bool haveCur, anyhit, finite;
 };
+
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 // Traversal stack of one lane: entries [0, KL) in LDS at lds[j * TL_LANES] ([entry][lane], the
 // block is always 256 lanes, so addresses are shifts), deeper ones in the global overflow
@@ -223,8 +219,8 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
       continue;
     }
     float e1, e2;
-    const float d1 = slab(L.o, L.inv, mk3(g.b0.x, g.b0.y, g.b0.z), mk3(g.b0.w, g.b1.x, g.b1.y), e1);
-    const float d2 = slab(L.o, L.inv, mk3(g.b1.z, g.b1.w, g.b2.x), mk3(g.b2.y, g.b2.z, g.b2.w), e2);
+    const float d1 = slab(L.o(), L.inv(), mk3(g.b0.x, g.b0.y, g.b0.z), mk3(g.b0.w, g.b1.x, g.b1.y), e1);
+    const float d2 = slab(L.o(), L.inv(), mk3(g.b1.z, g.b1.w, g.b2.x), mk3(g.b2.y, g.b2.z, g.b2.w), e2);
     return aL == (d1 < d2);
   }
   return a < b;
@@ -237,18 +233,18 @@ RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
-  const float dn = dot(ng, L.d);
+  const float dn = dot(ng, L.d());
   if (fabs_(dn) < 0.00001f) return false;                           // RT:262
-  const float num = dot(ng, p1) - dot(L.o, ng);
+  const float num = dot(ng, p1) - dot(L.o(), ng);
   // Conservative early reject before the correctly rounded division: num * rcp(dn) is within
   // ~2^-21 of num / dn (|dn| >= 1e-5, no denormals), so outside these margins the exact t
   // fails RT:268 or the closest-hit test for certain.  NaN never rejects.
   const float qa = num * __builtin_amdgcn_rcpf(dn);
   if (qa < 0.0005f * (1.0f - 0x1p-16f) || qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
-  const float t = num / dot(L.d, ng);                                // RT:265
+  const float t = num / dot(L.d(), ng);                                // RT:265
   const float dist = t - 0.00001f;
   if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
-  const f3 Pp = L.o + L.d * t;
+  const f3 Pp = L.o() + L.d() * t;
   const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
   const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
   const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
@@ -285,8 +281,8 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
   const float4 b0 = ld<float4>(P.nodes, off), b1 = ld<float4>(P.nodes, off + 16u), b2 = ld<float4>(P.nodes, off + 32u);
   const int2 ref = ld<int2>(P.nodes, off + 48u);
   float e1, e2;
-  const float d1 = slab(L.o, L.inv, mk3(b0.x, b0.y, b0.z), mk3(b0.w, b1.x, b1.y), e1);
-  const float d2 = slab(L.o, L.inv, mk3(b1.z, b1.w, b2.x), mk3(b2.y, b2.z, b2.w), e2);
+  const float d1 = slab(L.o(), L.inv(), mk3(b0.x, b0.y, b0.z), mk3(b0.w, b1.x, b1.y), e1);
+  const float d2 = slab(L.o(), L.inv(), mk3(b1.z, b1.w, b2.x), mk3(b2.y, b2.z, b2.w), e2);
   int nearRef = 0;
   float nearE = 0.0f;
   bool descend = false;
@@ -310,27 +306,53 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
 // the reference's slab test; survivors sorted by entry distance, nearest entered, rest stacked
 RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
   const uint32_t off = (uint32_t)L.cur << 7;
-  const float4 lx = ld<float4>(P.qnodes, off), ly = ld<float4>(P.qnodes, off + 16u),
-               lz = ld<float4>(P.qnodes, off + 32u), hx = ld<float4>(P.qnodes, off + 48u),
-               hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
+  // t0 / t1 of RT:312-313 for the four children; the box is hit iff t1 >= t0 && t1 > 0,
+  // which is exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
   const int4 rf = ld<int4>(P.qnodes, off + 96u);
   const float lim = cull ? cull_limit(L.best) : __int_as_float(0x7f800000);
   float k[4];
   int r[4];
-  {
-    const float ax[4] = {lx.x, lx.y, lx.z, lx.w}, ay[4] = {ly.x, ly.y, ly.z, ly.w}, az[4] = {lz.x, lz.y, lz.z, lz.w};
-    const float bx[4] = {hx.x, hx.y, hx.z, hx.w}, by[4] = {hy.x, hy.y, hy.z, hy.w}, bz[4] = {hz.x, hz.y, hz.z, hz.w};
-    const int rr[4] = {rf.x, rf.y, rf.z, rf.w};
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      float e;
-      const float dd = slab(L.o, L.inv, mk3(ax[c], ay[c], az[c]), mk3(bx[c], by[c], bz[c]), e);
-      const bool ok = dd > 0 && !(e > lim);
-      k[c] = ok ? e : __int_as_float(0x7f800000);
-      r[c] = ok ? rr[c] : Q_EMPTY;
-    }
+  auto keep = [&](int c, float t0, float t1, int ref) {
+    const bool ok = t1 >= t0 && t1 > 0.0f && !(t0 > lim);
+    k[c] = ok ? t0 : __int_as_float(0x7f800000);
+    r[c] = ok ? ref : Q_EMPTY;
+  };
+  if (L.finite) {
+    // near / far planes chosen per ray by the load offsets; children in pairs with packed
+    // fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations, two at a time)
+    const float4 nx = ld<float4>(P.qnodes, off + L.offNx), ny = ld<float4>(P.qnodes, off + L.offNy),
+                 nz = ld<float4>(P.qnodes, off + L.offNz);
+    const float4 fx = ld<float4>(P.qnodes, off + (48 - L.offNx)), fy = ld<float4>(P.qnodes, off + (80 - L.offNy)),
+                 fz = ld<float4>(P.qnodes, off + (112 - L.offNz));
+    const v2f ox = {L.ox, L.ox}, oy = {L.oy, L.oy}, oz = {L.oz, L.oz};
+    const v2f ix = {L.ix, L.ix}, iy = {L.iy, L.iy}, iz = {L.iz, L.iz};
+    const v2f nx01 = (v2f{nx.x, nx.y} - ox) * ix, ny01 = (v2f{ny.x, ny.y} - oy) * iy, nz01 = (v2f{nz.x, nz.y} - oz) * iz;
+    const v2f nx23 = (v2f{nx.z, nx.w} - ox) * ix, ny23 = (v2f{ny.z, ny.w} - oy) * iy, nz23 = (v2f{nz.z, nz.w} - oz) * iz;
+    const v2f fx01 = (v2f{fx.x, fx.y} - ox) * ix, fy01 = (v2f{fy.x, fy.y} - oy) * iy, fz01 = (v2f{fz.x, fz.y} - oz) * iz;
+    const v2f fx23 = (v2f{fx.z, fx.w} - ox) * ix, fy23 = (v2f{fy.z, fy.w} - oy) * iy, fz23 = (v2f{fz.z, fz.w} - oz) * iz;
+    keep(0, max_(nx01.x, max_(ny01.x, nz01.x)), min_(fx01.x, min_(fy01.x, fz01.x)), rf.x);
+    keep(1, max_(nx01.y, max_(ny01.y, nz01.y)), min_(fx01.y, min_(fy01.y, fz01.y)), rf.y);
+    keep(2, max_(nx23.x, max_(ny23.x, nz23.x)), min_(fx23.x, min_(fy23.x, fz23.x)), rf.z);
+    keep(3, max_(nx23.y, max_(ny23.y, nz23.y)), min_(fx23.y, min_(fy23.y, fz23.y)), rf.w);
+  } else {  // a direction component is exactly 0: the literal slab (0 * inf -> NaN cases)
+    const float4 lx = ld<float4>(P.qnodes, off), ly = ld<float4>(P.qnodes, off + 16u),
+                 lz = ld<float4>(P.qnodes, off + 32u), hx = ld<float4>(P.qnodes, off + 48u),
+                 hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
+    auto generic = [&](int c, float ax, float ay, float az, float bx, float by, float bz, int ref) {
+      const f3 f = (mk3(bx, by, bz) - L.o()) * L.inv();
+      const f3 n = (mk3(ax, ay, az) - L.o()) * L.inv();
+      keep(c, max_(min_(f.x, n.x), max_(min_(f.y, n.y), min_(f.z, n.z))),
+           min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z))), ref);
+    };
+    generic(0, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, rf.x);
+    generic(1, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, rf.y);
+    generic(2, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, rf.z);
+    generic(3, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, rf.w);
   }
   const int n = (r[0] != Q_EMPTY) + (r[1] != Q_EMPTY) + (r[2] != Q_EMPTY) + (r[3] != Q_EMPTY);
+  // valid children sort ahead of empty slots unless a valid entry key is +inf (degenerate)
+  const bool ordered = !((r[0] != Q_EMPTY && !(k[0] < INFINITY)) || (r[1] != Q_EMPTY && !(k[1] < INFINITY)) ||
+                         (r[2] != Q_EMPTY && !(k[2] < INFINITY)) || (r[3] != Q_EMPTY && !(k[3] < INFINITY)));
   // 5-comparator sorting network on (entry, ref); empty slots (key +inf) sink to the end
 #define RT_CSWAP(a, b)                                      \
   {                                                         \
@@ -345,7 +367,7 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   // a +inf key can only be a valid child in degenerate cases; keep the entry count exact
   const int2 e1 = make_int2(r[1], __float_as_int(k[1])), e2 = make_int2(r[2], __float_as_int(k[2])),
              e3 = make_int2(r[3], __float_as_int(k[3]));
-  if (L.sp + 3 <= S.KL && r[0] != Q_EMPTY && (n < 2 || r[n - 1] != Q_EMPTY)) {
+  if (L.sp + 3 <= S.KL && n > 0 && ordered) {
     // branch-free: the far-to-near entries 3, 2, 1 land at sp, sp+[n>=4], sp+[n>=4]+[n>=3];
     // an empty entry is overwritten by the next write, so exactly n-1 entries survive
     const int a0 = L.sp, a1 = a0 + (n >= 4), a2 = a1 + (n >= 3);
@@ -401,7 +423,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   int entry = 0, parked = 0;
   bool haveParked = false;
   TraceLane L;
-  L.o = L.d = L.inv = splat(0.0f);
+  L.ox = L.oy = L.oz = L.dx = L.dy = L.dz = L.ix = L.iy = L.iz = 0.0f;
   L.best = INF; L.bestt = 0.0f; L.besttri = -1;
   L.sp = L.cur = L.tri_i = L.tri_end = 0;
   L.haveCur = L.anyhit = false;
@@ -437,9 +459,15 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
           L.anyhit = (entry & 1) != 0;
           const float4 oo = L.anyhit ? S.so[path] : S.ro[path];
           const float4 dd = L.anyhit ? S.sd[path] : S.rd[path];
-          L.o = mk3(oo.x, oo.y, oo.z);
-          L.d = mk3(dd.x, dd.y, dd.z);
-          L.inv = mk3(1.0f / L.d.x, 1.0f / L.d.y, 1.0f / L.d.z);
+          L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
+          L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+          L.ix = 1.0f / L.dx; L.iy = 1.0f / L.dy; L.iz = 1.0f / L.dz;
+          // finite 1/d: per axis (lo-o)*inv <= (hi-o)*inv exactly when inv > 0 (rounding is
+          // monotone), so the slab min/max of RT:309-310 is a fixed choice of plane per ray
+          L.finite = fabs_(L.ix) < INFINITY && fabs_(L.iy) < INFINITY && fabs_(L.iz) < INFINITY;
+          L.offNx = L.ix > 0.0f ? 0 : 48;
+          L.offNy = L.iy > 0.0f ? 16 : 64;
+          L.offNz = L.iz > 0.0f ? 32 : 80;
           L.best = INF;
           L.besttri = -1;
           L.bestt = 0.0f;
@@ -546,8 +574,20 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
 }
 
 // ----------------------------------------------------------------------------- shade
-__global__ __launch_bounds__(256) void wf_shade(const WFParams W) {
-  __shared__ unsigned int sm[8];
+// Paths per block-iteration of wf_shade = 256 x SH_SUB: the block stages its queue / active
+// entries in LDS and claims global space with one atomic per list per 1024 paths.
+#ifndef RT_SH_SUB
+#define RT_SH_SUB 4
+#endif
+#ifndef RT_SHADE_WPE
+#define RT_SHADE_WPE 1
+#endif
+constexpr int SH_SUB = RT_SH_SUB;
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
+  __shared__ int lq[2 * 256 * SH_SUB];
+  __shared__ int la[256 * SH_SUB];
+  __shared__ unsigned int lc[4];  // queue count, active count, queue base, active base
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
@@ -557,8 +597,11 @@ __global__ __launch_bounds__(256) void wf_shade(const WFParams W) {
   const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
-  for (unsigned int base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
-    const unsigned int idx = base + threadIdx.x;
+  for (unsigned int base = blockIdx.x * (256u * SH_SUB); base < na; base += gridDim.x * (256u * SH_SUB)) {
+  if (threadIdx.x == 0) lc[0] = lc[1] = 0u;
+  __syncthreads();
+  for (int sub = 0; sub < SH_SUB; sub++) {
+    const unsigned int idx = base + (unsigned)sub * 256u + threadIdx.x;
     const bool live = idx < na;
     int path = live ? S.active[in][idx] : 0;
     bool doFinish = false, doBounce = false;
@@ -761,11 +804,21 @@ __global__ __launch_bounds__(256) void wf_shade(const WFParams W) {
         S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
       }
     }
-    const unsigned int qs = block_append(&S.cnt[out], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u), sm);
-    if (qShadow) S.queue[out][qs] = (path << 1) | 1;
-    if (qCont) S.queue[out][qs + (qShadow ? 1u : 0u)] = path << 1;
-    const unsigned int ai = block_append(&S.cnt[2 + out], keep ? 1u : 0u, sm);
-    if (keep) S.active[out][ai] = path;
+    const unsigned int qs = wave_lds_append(&lc[0], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u));
+    if (qShadow) lq[qs] = (path << 1) | 1;
+    if (qCont) lq[qs + (qShadow ? 1u : 0u)] = path << 1;
+    const unsigned int ai = wave_lds_append(&lc[1], keep ? 1u : 0u);
+    if (keep) la[ai] = path;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    lc[2] = lc[0] ? atomicAdd(&S.cnt[out], lc[0]) : 0u;
+    lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
+  }
+  __syncthreads();
+  for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue[out][lc[2] + j] = lq[j];
+  for (unsigned int j = threadIdx.x; j < lc[1]; j += 256u) S.active[out][lc[3] + j] = la[j];
+  __syncthreads();
   }
   // per-wave counter flush
   for (int off = 32; off > 0; off >>= 1) {

@@ -9,6 +9,7 @@ raises ``RuntimeError``.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import dataclasses
 from typing import Optional, Sequence
 
@@ -118,7 +119,7 @@ _lib = None
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
-        L = C.CDLL(str(lib_path("librtamd.so")))
+        L = C.CDLL(os.environ.get("RTAMD_LIB") or str(lib_path("librtamd.so")))
         vp = C.c_void_p
         L.rt_create.argtypes = [C.c_int, C.POINTER(vp)]
         L.rt_destroy.argtypes = [vp]
