@@ -468,6 +468,119 @@ RTD f3 DisneySample(float xi_1, float xi_2, float xi_3, const Mat& material, f3 
   return f * fabs_(dot(N, L));
 }
 
+// ----------------------------------------------------------- BRDF mode (enableBSDF == false)
+RTD float GTR2(float NdotH, float alpha) {  // RT:441-445
+  float a2 = alpha * alpha;
+  float t = 1 + (a2 - 1) * NdotH * NdotH;
+  return a2 / (PI * t * t);
+}
+RTD void CalculateBRDFLobePdfs(const Mat& m, float& pDiffuse, float& pSpecular, float& pClearcoat) {  // RT:520-533
+  float r_diffuse = (1.0f - m.metallic);
+  float r_specular = (1.0f - m.metallic) + m.metallic;
+  float r_clearcoat = (1.0f - m.metallic) * 0.25f * m.clearcoat;
+  float r_sum_inv = 1.0f / (r_diffuse + r_specular + r_clearcoat);
+  pDiffuse = r_diffuse * r_sum_inv;
+  pSpecular = r_specular * r_sum_inv;
+  pClearcoat = r_clearcoat * r_sum_inv;
+}
+RTD f3 toNormalHemisphere(f3 v, f3 N) {  // RT:663-669
+  f3 helper = mk3(1, 0, 0);
+  if (fabs_(N.x) > 0.999f) helper = mk3(0, 0, 1);
+  f3 tangent = normalize(cross(N, helper));
+  f3 bitangent = normalize(cross(N, tangent));
+  return v.x * tangent + v.y * bitangent + v.z * N;
+}
+RTD f3 SampleCosineHemisphere(float xi_1, float xi_2, f3 N) {  // RT:673-685
+  float r = sqrt_(xi_1);
+  float theta = xi_2 * TWO_PI;
+  float x = r * cos_(theta);
+  float y = r * sin_(theta);
+  float z = sqrt_(1.0f - x * x - y * y);
+  return toNormalHemisphere(mk3(x, y, z), N);
+}
+RTD f3 SampleGTR1_h(float xi_1, float xi_2, f3 V, f3 N, float alpha) {  // RT:697-714
+  float phi_h = xi_1 * TWO_PI;
+  float sin_phi_h = sin_(phi_h);
+  float cos_phi_h = cos_(phi_h);
+  float cos_theta_h = sqrt_((1.0f - pow_(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
+  float sin_theta_h = sqrt_(max_(0.0f, 1.0f - cos_theta_h * cos_theta_h));
+  f3 H = mk3(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
+  H = toNormalHemisphere(H, N);
+  return reflect(-V, H);
+}
+RTD f3 SampleGTR2(float xi_1, float xi_2, f3 V, f3 N, float alpha) {  // RT:732-749
+  float phi_h = 2.0f * PI * xi_1;
+  float sin_phi_h = sin_(phi_h);
+  float cos_phi_h = cos_(phi_h);
+  float cos_theta_h = sqrt_((1.0f - xi_2) / (1.0f + (alpha * alpha - 1.0f) * xi_2));
+  float sin_theta_h = sqrt_(max_(0.0f, 1.0f - cos_theta_h * cos_theta_h));
+  f3 H = mk3(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
+  H = toNormalHemisphere(H, N);
+  return reflect(-V, H);
+}
+RTD f3 SampleBRDF(float xi_1, float xi_2, float xi_3, f3 V, f3 N, const Mat& m) {  // RT:789-833
+  float p_diffuse, p_specular, p_clearcoat;
+  CalculateBRDFLobePdfs(m, p_diffuse, p_specular, p_clearcoat);
+  float alpha_GTR1 = mix_(0.1f, 0.001f, m.clearcoatGloss);
+  float alpha_GTR2 = max_(0.001f, sqr(m.roughness));
+  float cdf0 = p_diffuse;
+  float cdf1 = cdf0 + p_clearcoat;
+  float cdf2 = cdf1 + p_specular;
+  // RT:808-817 compute an eta, a VNDF half vector and a Fresnel that are never used
+  if (xi_3 <= cdf0) return SampleCosineHemisphere(xi_1, xi_2, N);
+  else if (xi_3 <= cdf1) return SampleGTR1_h(xi_1, xi_2, V, N, alpha_GTR1);
+  else if (xi_3 <= cdf2) return SampleGTR2(xi_1, xi_2, V, N, alpha_GTR2);
+  return mk3(0, 1, 0);
+}
+RTD f3 BRDF_Evaluate(f3 V, f3 N, f3 L, f3 X, f3 Y, const Mat& m, float& pdf) {  // RT:836-921
+  pdf = 1e-10f;
+  float NdotL = dot(N, L);
+  float NdotV = dot(N, V);
+  if (NdotL < 0 || NdotV < 0) return splat(0.0f);
+  f3 H = normalize(L + V);
+  float NdotH = dot(N, H);
+  float LdotH = dot(L, H);
+  f3 Cdlin = m.baseColor;
+  float Cdlum = Luminance(Cdlin);
+  f3 Ctint = (Cdlum > 0) ? (Cdlin / Cdlum) : splat(1.0f);
+  f3 Cspec = m.specular * mix(splat(1.0f), Ctint, m.specularTint);
+  f3 Cspec0 = mix(0.08f * Cspec, Cdlin, m.metallic);
+  f3 Csheen = mix(splat(1.0f), Ctint, m.sheenTint);
+  float Fd90 = 0.5f + 2.0f * LdotH * LdotH * m.roughness;
+  float FL = SchlickFresnel(NdotL);
+  float FV = SchlickFresnel(NdotV);
+  float Fd = mix_(1.0f, Fd90, FL) * mix_(1.0f, Fd90, FV);
+  float Fss90 = LdotH * LdotH * m.roughness;
+  float Fss = mix_(1.0f, Fss90, FL) * mix_(1.0f, Fss90, FV);
+  float ss = 1.25f * (Fss * (1.0f / (NdotL + NdotV) - 0.5f) + 0.5f);
+  float FH = SchlickFresnel(LdotH);
+  float alpha = max_(0.001f, sqr(m.roughness));
+  float Ds = GTR2(NdotH, alpha);
+  f3 Fs = mix(Cspec0, splat(1.0f), FH);
+  float Gs = SmithG_GGX(NdotL, m.roughness);  // R27: roughness, not alpha
+  Gs *= SmithG_GGX(NdotV, m.roughness);
+  if (m.anisotropic > 0) {
+    Ds = GTR2_Aniso(NdotH, dot(H, X), dot(H, Y), m.ax, m.ay);
+    Gs = SmithG_GGX_Aniso(NdotL, dot(L, X), dot(L, Y), m.ax, m.ay);
+    Gs *= SmithG_GGX_Aniso(NdotV, dot(V, X), dot(V, Y), m.ax, m.ay);
+  }
+  float Dr = GTR1(NdotH, mix_(0.1f, 0.001f, 1.0f - m.clearcoatGloss));
+  float Fr = mix_(0.04f, 1.0f, FH);
+  float Gr = SmithG_GGX(NdotL, 0.25f) * SmithG_GGX(NdotV, 0.25f);
+  f3 Fsheen = FH * m.sheen * Csheen;
+  f3 diffuse = INV_PI * mix_(Fd, ss, m.subsurface) * Cdlin + Fsheen;
+  f3 specular = Gs * Fs * Ds / (4.0f * NdotV * NdotL);
+  f3 clearcoat = splat(0.25f) * Gr * Fr * Dr * m.clearcoat / (4.0f * NdotV * NdotL);
+  float p_diffuse, p_specular, p_clearcoat;
+  CalculateBRDFLobePdfs(m, p_diffuse, p_specular, p_clearcoat);
+  float pdf_diffuse = NdotL * INV_PI;
+  float pdf_specular = Ds * NdotH / (4.0f * LdotH);
+  float pdf_clearcoat = Dr * NdotH / (4.0f * LdotH);
+  pdf = p_diffuse * pdf_diffuse + p_specular * pdf_specular + p_clearcoat * pdf_clearcoat;
+  pdf = max_(1e-10f, pdf);
+  return (1.0f - m.metallic) * diffuse + specular + clearcoat;
+}
+
 RTD f3 SampleHG(f3 V, float g, float r1, float r2) {  // RT:1195-1216
   float cosTheta;
   if (fabs_(g) < 0.001f) cosTheta = 1 - 2 * r2;

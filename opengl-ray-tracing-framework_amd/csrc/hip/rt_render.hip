@@ -674,6 +674,8 @@ int rt_clear_accum(rt_ctx* c) {
 int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames) {
   if (!c || !fp || n_frames < 0 || (n_frames && !rand_origin)) return RT_ERR_ARG;
   if (!c->scene_set || !c->env_set || !c->frame_set) return fail(c, RT_ERR_STATE, "set_scene, set_env and resize first");
+  if ((fp->flags & RT_FLAG_MEGAKERNEL) && !fp->enable_bsdf)
+    return fail(c, RT_ERR_ARG, "BRDF mode (enable_bsdf = 0) runs on the wavefront path only");
   HIPCHK(c, hipSetDevice(c->device));
   if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
     const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
@@ -794,8 +796,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             HIPCHK(c, hipEventElapsedTime(&ms, t0, t1));
             HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
             HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
-            fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu max %llu\n",
-                    g, pass, q[0], ms, h[2], h[3], h[4], h[5], h[6]);
+            fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
+                    "wave-iters max %llu ray-steps max %llu\n", g, pass, q[0], ms, h[2], h[3], h[4], h[5], h[6], h[7]);
+            HIPCHK(c, hipMemset(c->d_stats + 6, 0, 2 * sizeof(unsigned long long)));
           }
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));

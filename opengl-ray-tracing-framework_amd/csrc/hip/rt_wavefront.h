@@ -428,6 +428,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   L.sp = L.cur = L.tri_i = L.tri_end = 0;
   L.haveCur = L.anyhit = false;
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
+  unsigned int ray_steps = 0, ray_steps_max = 0;  // COUNT: node + triangle steps of the lane's ray
 
   while (true) {
     if (COUNT) v_iter++;
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
             L.tri_end = L.tri_i + leaf_count(L.cur);
             L.haveCur = false;
           } else {
-            if (COUNT) v_int++;
+            if (COUNT) { v_int++; ray_steps++; }
             if (WIDE) tl_qnode(P, L, TS, cull);
             else tl_node(P, L, TS, cull);
           }
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
             if (MODE == TM_WW) L.haveCur = false;
             else L.haveCur = tl_pop(L, TS, cull);
           } else {
-            if (COUNT) v_int++;
+            if (COUNT) { v_int++; ray_steps++; }
             if (WIDE) tl_qnode(P, L, TS, cull);
             else tl_node(P, L, TS, cull);
           }
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
       while (__any(L.tri_i < L.tri_end)) {
         if (COUNT) v_iter++;
         if (L.tri_i < L.tri_end) {
-          if (COUNT) v_tri++;
+          if (COUNT) { v_tri++; ray_steps++; }
           if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
             finished = true;
             L.tri_end = L.tri_i;
@@ -554,6 +555,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
     }
     if (busy && finished) {
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
+      if (COUNT) { ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; }
       busy = false;
     }
   }
@@ -569,6 +571,10 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
       atomicAdd(&P.stats[4], v_tri);
       atomicAdd(&P.stats[5], v_iter);
       atomicMax(&P.stats[6], v_iter);
+    }
+    for (int off = 32; off > 0; off >>= 1) ray_steps_max = max(ray_steps_max, (unsigned)__shfl_xor((int)ray_steps_max, off));
+    if ((threadIdx.x & 63) == 0) {
+      atomicMax(&P.stats[7], (unsigned long long)ray_steps_max);
     }
   }
 }
@@ -662,9 +668,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
             Lo = splat(0.0f);
             hist = splat(1.0f);
             bounce = 0;
-          } else {  // RT:1509-1510
+          } else if (P.enable_bsdf) {  // RT:1509-1510
             const f3 Le = xyz(P.mats[8 * nmat]);
             Lo = Lo + hist * Le * evf / evp;
+            bounce++;
+          } else {  // BRDF mode RT:1362-1364 (evf = f_r, evp = pdf_brdf, s4.x = N.L)
+            const f3 Le = xyz(P.mats[8 * nmat]);
+            Lo = Lo + hist * Le * evf * fabs_(S.s4[path].x) / evp;
             bounce++;
           }
           hP = Pp;
@@ -676,6 +686,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
           else { fin = Le0 + Lo; doFinish = true; }
         } else if (flags & PF_CAMERA) {  // RT:1532-1539
           fin = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
+          doFinish = true;
+        } else if (!P.enable_bsdf) {  // BRDF mode RT:1345-1359
+          const float aNdotL = fabs_(S.s4[path].x);
+          if (P.enable_env) {
+            f3 skyColor;
+            float pdf_light;
+            hdrColorPdf(E, rd, skyColor, pdf_light);
+            skyColor = skyColor * E.intensity;
+            const float mis_weight = misMixWeight(evp, pdf_light);
+            Lo = Lo + mis_weight * hist * skyColor * evf * aNdotL / evp;
+          } else {
+            const f3 skyColor = getDefaultSkyColor(rd.y);
+            Lo = Lo + hist * skyColor * evf * aNdotL / evp;
+          }
+          fin = Le0 + Lo;
           doFinish = true;
         } else {  // RT:1483-1506
           if (P.enable_env) {
@@ -701,7 +726,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     f3 cnee = splat(0.0f), cmed = splat(0.0f);
     uint32_t nflags = 0;
     f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
-    if (doBounce) {
+    float bNdotL = 0.0f;  // BRDF mode: N.L of the sampled direction (RT:1336)
+    if (doBounce && !P.enable_bsdf) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
+      const Mat m = load_mat(P.mats, mat);
+      const f3 V = -hV, N = hN;
+      const float xa = rand_(wseed);
+      const float xb = rand_(wseed);
+      const f3 Ll = SampleHdr(E, xa, xb);
+      f3 T, Bt;
+      getTangent(N, T, Bt);
+      if (dot(N, Ll) > 0.0f) {
+        f3 light_fr;
+        float light_pdf;
+        hdrColorPdf(E, Ll, light_fr, light_pdf);
+        light_fr = light_fr * E.intensity;
+        float brdf_pdf;
+        const f3 brdf_fr = BRDF_Evaluate(V, N, Ll, T, Bt, m, brdf_pdf);
+        const float mis_weight = misMixWeight(light_pdf, brdf_pdf);
+        cnee = mis_weight * hist * light_fr * brdf_fr * fabs_(dot(N, Ll)) / light_pdf;
+        shO = hP;
+        shD = Ll;
+        qShadow = true;
+        nflags |= PF_SHADOW;
+      }
+      int g = P.loop_num[frame] + 1;
+      g = g ^ (g >> 1);
+      float sx = sobol_gray((int)bounce * 2, g);
+      float sy = sobol_gray((int)bounce * 2 + 1, g);
+      const float cu = rand_(wseed), cv = rand_(wseed);
+      sx += cu;
+      if (sx > 1) sx -= 1;
+      if (sx < 0) sx += 1;
+      sy += cv;
+      if (sy > 1) sy -= 1;
+      if (sy < 0) sy += 1;
+      const float xi_3 = rand_(wseed);
+      const f3 L = SampleBRDF(sx, sy, xi_3, V, N, m);
+      bNdotL = dot(N, L);
+      float pdf_brdf;
+      const f3 f_r = BRDF_Evaluate(V, N, L, T, Bt, m, pdf_brdf);
+      if (pdf_brdf > 0.0f) {
+        hist = hist * (f_r * fabs_(bNdotL) / pdf_brdf);
+        evf = f_r;
+        evp = pdf_brdf;
+        contO = hP;
+        contD = L;
+        qCont = true;
+        nflags |= PF_CONT;
+      }
+      if (!qShadow && !qCont) {
+        fin = Le0 + Lo;
+        doFinish = true;
+      }
+    } else if (doBounce) {
       const Mat m = load_mat(P.mats, mat);
       const f3 V = -hV;
       // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
@@ -794,6 +871,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
       S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
       if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
+      if (!P.enable_bsdf && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
       S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
       if (qCont) {
         S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);

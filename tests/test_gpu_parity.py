@@ -95,3 +95,36 @@ def test_binary_wavefront_traversal_matches(gpu_renderer, env_maps, monkeypatch)
     monkeypatch.setenv("RT_BVH_WIDTH", "2")
     img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("env,mis", [(True, True), (True, False), (False, True)], ids=["env-mis", "env-nomis", "sky"])
+@pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
+def test_brdf_mode_matches_oracle_bitwise(gpu_renderer, env_maps, name, env, mis):
+    """enableBSDF = false: shadingImportanceSampling_BRDF (RT:1290-1367) on the wavefront path."""
+    sd = cf.config_scene(name)
+    W, H = 64, 36
+    fp = cf.frame_params(W, H, enable_bsdf=False, enable_env_map=env, enable_mis=mis)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_megakernel_rejects_brdf_mode(gpu_renderer, env_maps):
+    sd = cf.config_scene("C2")
+    fp = cf.frame_params(32, 32, enable_bsdf=False, flags=RT_FLAG_MEGAKERNEL)
+    with pytest.raises(RuntimeError, match="wavefront path only"):
+        gpu_render(gpu_renderer, sd, env_maps, 32, 32, fp, cf.rand_origins(1))
+
+
+@pytest.mark.parametrize("env,mis", [(False, True), (True, False)], ids=["sky", "env-nomis"])
+def test_bsdf_mode_env_and_mis_switches(gpu_renderer, env_maps, env, mis):
+    """enableEnvMap / enableMultiImportantSample off in BSDF mode (RT:1383-1405, 1483-1506)."""
+    sd = cf.config_scene("C4")
+    W, H = 64, 36
+    fp = cf.frame_params(W, H, enable_env_map=env, enable_mis=mis)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert bit_mismatch(img, ref)[0] == 0.0
