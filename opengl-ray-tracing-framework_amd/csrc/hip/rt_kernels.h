@@ -439,4 +439,11 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, float* _
   frame[o + 2] = c.z;
 }
 
+// rt_update_materials: the material id lives in .w of each triangle's first normal texel
+__global__ __launch_bounds__(256) void rt_set_material_kernel(float4* __restrict__ trin, int first, int count,
+                                                             int id) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) trin[3 * (size_t)(first + i)].w = __int_as_float(id);
+}
+
 }  // namespace rtd

@@ -565,11 +565,11 @@ int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_materi
     int rc = upload(c, (void**)&c->d_mats, c->mat_table.data(), c->mat_table.size() * sizeof(float));
     if (rc) return rc;
   }
-  for (int i = first; i < first + count; i++) {
-    c->tri_mat[i] = id;
-    // only the .w of the first normal texel carries the id: patch it in place
-    HIPCHK(c, hipMemcpyAsync(reinterpret_cast<char*>(c->d_trin + 3 * (size_t)i) + 12, &id, 4, hipMemcpyHostToDevice,
-                             c->stream));
+  for (int i = first; i < first + count; i++) c->tri_mat[i] = id;
+  if (count > 0) {
+    hipLaunchKernelGGL(rtd::rt_set_material_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream,
+                       c->d_trin, first, count, id);
+    HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return RT_OK;

@@ -116,9 +116,21 @@ class FrameParams:
 _lib = None
 
 
+def _share_torch_hip_runtime() -> None:
+    """PyTorch-ROCm ships its own libamdhip64.so with the system's soname (libamdhip64.so.7);
+    whichever is loaded first serves the whole process, and torch cannot run on the system one.
+    Loading torch first makes librtamd.so bind to torch's runtime, so device pointers can be
+    exchanged with torch tensors (bench.py's RCCL gather) in either import order."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
+        _share_torch_hip_runtime()
         L = C.CDLL(os.environ.get("RTAMD_LIB") or str(lib_path("librtamd.so")))
         vp = C.c_void_p
         L.rt_create.argtypes = [C.c_int, C.POINTER(vp)]

@@ -1,0 +1,151 @@
+"""GPU tests of the C-ABI semantics around the kernel (include/rt_abi.h): progressive
+accumulation across calls, history written by the host, the maxIterations cap (R12),
+material updates, odd frame / tile sizes, an empty scene, and the multi-rank tile split with
+the device-side frame assembly.  Every image is checked bit for bit against the oracle."""
+import numpy as np
+import pytest
+
+from helpers import bit_mismatch, frames_for, gpu_render, oracle_render
+from rtamd import configs as cf
+from rtamd import scene_lib as sl
+from rtamd import tiling
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene_from(s: sl.Scene) -> cf.SceneData:
+    tri, nodes = s.encode()
+    return cf.SceneData("custom", s.counts(), tri, nodes, s.export_soa(), s.nodes(), [])
+
+
+def test_progressive_accumulation_across_calls(gpu_renderer, env_maps):
+    """Frames 1-2 in one call and 3-5 in the next == frames 1-5 (main.cpp:175-200 LoopNum)."""
+    sd = cf.config_scene("C2")
+    W, H = 48, 32
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 5)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    r = gpu_renderer
+    gpu_render(r, sd, env_maps, W, H, fp, ro[:2])
+    r.render(fp, ro[2:])
+    assert r.loop_num == 5
+    assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
+
+
+def test_host_written_history_and_loop_num(gpu_renderer, env_maps):
+    """rt_write_accum + rt_set_loop_num resume a progressive render from a given history."""
+    sd = cf.config_scene("C3")
+    W, H = 40, 24
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 4)
+    hist, _ = oracle_render(sd, env_maps, W, H, frames[:2])
+    ref, _ = oracle_render(sd, env_maps, W, H, frames[2:], accum=hist)
+    img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro[2:], accum=hist, loop_num=2)
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_max_iterations_caps_progression(gpu_renderer, env_maps):
+    """maxIterations = 3: LoopNum stops at 3 and frames at the cap trace nothing (R12)."""
+    sd = cf.config_scene("C2")
+    W, H = 32, 32
+    fp = cf.frame_params(W, H, max_iterations=3)
+    ro = cf.rand_origins(6)
+    # host logic of main.cpp:175-178 over six frames: loop 1, 2 traced, then 3, 3, 3, 3 untraced
+    frames, loop = [], 0
+    for k in range(6):
+        if loop < 3:
+            loop += 1
+        if loop < 3:
+            frames.append(cf.oracle_frame_params(fp, loop, ro[k]))
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert gpu_renderer.loop_num == 3
+    assert st["samples"] == cnt["samples"] == 2 * W * H
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_update_materials_matches_reencoded_scene(gpu_renderer, env_maps):
+    """rt_update_materials (RefreshTriangleMaterial) == re-encoding the scene with the material."""
+    s = sl.Scene()
+    for o in cf.CONFIGS["C2"].objects:
+        s.add_mesh(cf.load_mesh(o.mesh), cf.MATERIALS[o.material], o.rotate, o.translate, o.scale, o.smooth)
+    s.build_bvh(8)
+    before = _scene_from(s)
+    n = before.counts["n_triangles"]
+    new = cf.MATERIALS["golden"]
+    first, count = n // 3, n // 2  # a post-BVH range (rt_abi.h: indices after the BVH sort)
+    s.set_material(first, count, new)
+    after = _scene_from(s)
+    W, H = 48, 32
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(after, env_maps, W, H, frames)
+    r = gpu_renderer
+    r.set_scene_soa(before.soa, before.nodes)
+    r.update_materials(first, count, new.texels())
+    r.set_env(env_maps[0], env_maps[1])
+    r.resize(W, H)
+    r.set_loop_num(0)
+    r.render(fp, ro)
+    assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("W,H,tile", [(37, 23, 16), (70, 9, 32), (1, 1, 8)])
+def test_odd_frame_and_tile_sizes(gpu_renderer, env_maps, W, H, tile):
+    sd = cf.config_scene("C4")
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro, tile=tile)
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_empty_scene_renders_the_environment(gpu_renderer, env_maps):
+    s = sl.Scene()
+    s.build_bvh(8)
+    sd = _scene_from(s)
+    W, H = 32, 16
+    for env in (True, False):
+        fp = cf.frame_params(W, H, enable_env_map=env)
+        ro, frames = frames_for(fp, 1, 1)
+        ref, _ = oracle_render(sd, env_maps, W, H, frames)
+        img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+        assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
+    """Ranks r = 0..world-1 render their interleaved tiles (one context each, as one process per
+    GPU would); the rank-major concatenation of their device tile buffers, un-permuted by
+    rt_assemble_frame on the device, is the single-rank frame bit for bit (and the oracle's)."""
+    import torch
+    from rtamd.renderer import Renderer
+    sd = cf.config_scene("C3")
+    W, H, T = 80, 45, 16
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    parts = []
+    ctxs = [gpu_renderer] + [Renderer(0) for _ in range(world - 1)]
+    try:
+        for rank, r in enumerate(ctxs):
+            gpu_render(r, sd, env_maps, W, H, fp, ro, tile=T, rank=rank, world=world)
+            info = r.accum_device()
+            buf = torch.empty(info["bytes"] // 4, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()  # buf allocated on torch's stream, copied on the ctx stream
+            r.copy_accum_device(buf.data_ptr(), info["bytes"])
+            r.synchronize()
+            parts.append(buf)
+        gathered = torch.cat(parts)
+        torch.cuda.synchronize()
+        frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+        ctxs[0].assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
+        torch.cuda.synchronize()
+        img = frame.cpu().numpy().reshape(H, W, 3)
+        mlt = tiling.max_local_tiles(W, H, T, T, world)
+        host = tiling.assemble(gathered.cpu().numpy().reshape(world, mlt, T, T, 4), W, H, T, T, world)
+    finally:
+        for r in ctxs[1:]:
+            r.close()
+    assert bit_mismatch(img, ref)[0] == 0.0
+    assert bit_mismatch(host[..., :3], ref)[0] == 0.0
