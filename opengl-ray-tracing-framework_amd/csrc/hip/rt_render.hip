@@ -62,7 +62,8 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0;                          // wavefront traversal kernel
   int trace_lds_entries = 0, trace_lds = 0;
-  int trace_mode = 0;                         // rtd::TraceMode
+  int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
+  int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
   int pool_chunk = 256;                       // rays per queue atomic in wf_trace
   int2* d_stack_ovf = nullptr;
   size_t stack_ovf_bytes = 0;
@@ -238,8 +239,12 @@ int occupancy(rt_ctx* c) {
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
   bpc = 0;
-  c->trace_mode = rtd::TM_SPEC;
-  if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode = std::max(0, std::min(2, atoi(e)));
+  // measured per pass on C3: coherent camera rays prefer the speculative while-while schedule,
+  // incoherent secondary rays the dual-front one (tools/exp_dual2.sh)
+  c->trace_mode0 = rtd::TM_SPEC;
+  c->trace_mode = rtd::TM_DUAL;
+  if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode0 = c->trace_mode = std::max(0, std::min(3, atoi(e)));
+  if (const char* e = getenv("RT_TRACE_MODE0")) c->trace_mode0 = std::max(0, std::min(3, atoi(e)));
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256,
                                                          c->trace_lds));
   c->trace_bpc = std::max(1, bpc);
@@ -267,12 +272,15 @@ int occupancy(rt_ctx* c) {
 
 template <bool COUNT, bool WIDE>
 void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
-  switch (c->trace_mode) {
+  switch (WP.pass == 0 ? c->trace_mode0 : c->trace_mode) {
     case rtd::TM_IFIF:
       hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_IFIF, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
       break;
     case rtd::TM_WW:
       hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_WW, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
+      break;
+    case rtd::TM_DUAL:
+      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_DUAL, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
       break;
     default:
       hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_SPEC, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
@@ -352,8 +360,8 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
   c->own_stream = true;
   if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
-  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -789,7 +797,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           c->trace_events.push_back({t0, t1});
           c->trace_launches++;
           if (debug_passes) {  // development aid: per-pass rays / visits / duration (syncs!)
-            unsigned long long h[8];
+            unsigned long long h[16];
             unsigned int q[2];
             HIPCHK(c, hipStreamSynchronize(sg[g]));
             float ms = 0.0f;
@@ -798,7 +806,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
             fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
                     "wave-iters max %llu ray-steps max %llu\n", g, pass, q[0], ms, h[2], h[3], h[4], h[5], h[6], h[7]);
-            HIPCHK(c, hipMemset(c->d_stats + 6, 0, 2 * sizeof(unsigned long long)));
+            fprintf(stderr, "[rt]   lane utilisation: node phase %.3f (%llu iters)  tri phase %.3f (%llu iters)  busy at "
+                    "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
+                    h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
+            HIPCHK(c, hipMemset(c->d_stats + 6, 0, 10 * sizeof(unsigned long long)));
           }
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
@@ -877,7 +888,7 @@ int rt_stats_reset(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+  HIPCHK(c, hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
   c->kernel_ms = 0.0;
   c->launches = 0;
   c->trace_ms = 0.0;

@@ -165,7 +165,10 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
 //            every lane has a parked leaf (Aila & Laine's speculative traversal).
 // All three visit a superset-free subset of the reference's nodes and return the same closest
 // hit (culling only drops subtrees whose entry distance exceeds the best hit so far).
-enum TraceMode { TM_IFIF = 0, TM_WW = 1, TM_SPEC = 2 };
+//   TM_DUAL  every lane keeps a traversal cursor and a triangle cursor and each iteration advances
+//            both (one triangle of the current leaf + one node step); a lane waits only when it
+//            reaches a second leaf before finishing the first; idle lanes refill every iteration.
+enum TraceMode { TM_IFIF = 0, TM_WW = 1, TM_SPEC = 2, TM_DUAL = 3 };
 
 struct TraceLane {
   // ray as scalars (f3 members made SROA keep the lane in scratch memory)
@@ -429,6 +432,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   L.haveCur = L.anyhit = false;
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
   unsigned int ray_steps = 0, ray_steps_max = 0;  // COUNT: node + triangle steps of the lane's ray
+  unsigned long long v_itN = 0, v_itT = 0, v_itO = 0, v_park = 0, v_busyO = 0;  // COUNT: lane utilisation
 
   while (true) {
     if (COUNT) v_iter++;
@@ -483,8 +487,35 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
       }
     }
     if (!__any(busy)) break;
+    if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
-    if (MODE == TM_IFIF) {
+    if (MODE == TM_DUAL) {
+      if (COUNT) { v_itN++; v_itT++; }
+      if (busy) {
+        if (L.tri_i < L.tri_end) {
+          if (COUNT) { v_tri++; ray_steps++; }
+          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+            finished = true;
+            L.tri_end = L.tri_i;
+          }
+        }
+        if (!finished && L.haveCur) {
+          if (ref_is_leaf(L.cur)) {
+            if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
+              if (COUNT) { v_leaf++; v_park++; }
+              L.tri_i = leaf_first(L.cur);
+              L.tri_end = L.tri_i + leaf_count(L.cur);
+              L.haveCur = tl_pop(L, TS, cull);
+            }
+          } else {
+            if (COUNT) { v_int++; ray_steps++; }
+            if (WIDE) tl_qnode(P, L, TS, cull);
+            else tl_node(P, L, TS, cull);
+          }
+        }
+        if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
+      }
+    } else if (MODE == TM_IFIF) {
       if (busy) {
         if (L.tri_i < L.tri_end) {
           if (COUNT) v_tri++;
@@ -517,9 +548,10 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
           if (__all(!busy || !L.haveCur || haveParked)) break;
           act = busy && L.haveCur && !(haveParked && ref_is_leaf(L.cur));
         }
-        if (COUNT) v_iter++;
+        if (COUNT) { v_iter++; v_itN++; }
         if (act) {
           if (ref_is_leaf(L.cur)) {
+            if (COUNT) v_park++;
             parked = L.cur;
             haveParked = true;
             if (MODE == TM_WW) L.haveCur = false;
@@ -539,7 +571,7 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
         haveParked = false;
       }
       while (__any(L.tri_i < L.tri_end)) {
-        if (COUNT) v_iter++;
+        if (COUNT) { v_iter++; v_itT++; }
         if (L.tri_i < L.tri_end) {
           if (COUNT) { v_tri++; ray_steps++; }
           if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
@@ -564,6 +596,16 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
       v_int += __shfl_xor(v_int, off);
       v_leaf += __shfl_xor(v_leaf, off);
       v_tri += __shfl_xor(v_tri, off);
+      v_park += __shfl_xor(v_park, off);
+      v_busyO += __shfl_xor(v_busyO, off);
+    }
+    if ((threadIdx.x & 63) == 0) {  // wave-uniform iteration counts + lane-sums
+      atomicAdd(&P.stats[8], v_itN);
+      atomicAdd(&P.stats[9], v_int + v_park);
+      atomicAdd(&P.stats[10], v_itT);
+      atomicAdd(&P.stats[11], v_tri);
+      atomicAdd(&P.stats[12], v_itO);
+      atomicAdd(&P.stats[13], v_busyO);
     }
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&P.stats[2], v_int);
