@@ -54,6 +54,7 @@ struct KParams {
   float4* __restrict__ accum;
   unsigned int* __restrict__ counter;
   unsigned long long* __restrict__ stats;  // rays, samples, internal, leaf, tri
+  unsigned long long* __restrict__ wave_log;  // debug (RT_DEBUG_PASSES): per trace wave {t0, t1, iters, rays}
 };
 
 struct Visits {

@@ -65,6 +65,7 @@ struct rt_ctx {
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
   int pool_chunk = 256;                       // rays per queue atomic in wf_trace
+  int stagger = -1;                           // >= 0: group g starts after group g-1's pass `stagger` (measured slower)
   int2* d_stack_ovf = nullptr;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
@@ -309,7 +310,6 @@ hipEvent_t take_event(rt_ctx* c) {
   return e;
 }
 
-// Path-state buffers of the wavefront path, carved from one allocation.
 // Path-state buffers of the wavefront path: `paths` slots for each of the n_groups frame
 // groups, carved from one allocation (216 B per slot + counters).
 int alloc_wavefront(rt_ctx* c, size_t paths) {
@@ -360,6 +360,7 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
   c->own_stream = true;
   if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
+  if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
@@ -641,9 +642,11 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
   }
-  // frames in flight: path-state budget of 64M slots (216 B each, ~14 GB of the 288 GB HBM);
-  // the state grows on demand in rt_render_async, so interactive 1-frame use stays small
-  size_t max_slots = size_t(1) << 26;
+  // frames in flight: path-state budget of 160M slots (216 B each, ~35 GB of the 288 GB HBM:
+  // 64 frames at 1080p); the state grows on demand in rt_render_async, so interactive 1-frame
+  // use stays small.  More frames per launch amortise the per-pass latency floor of the few
+  // longest rays (C3: 16 frames 1.07, 32 frames 0.99, 64 frames 0.94 ms/frame).
+  size_t max_slots = size_t(160) << 20;
   if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
   c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / nv));
   int rc = alloc_wavefront(c, nv);
@@ -744,6 +747,12 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const int G = std::min(c->n_groups, nf);
       static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
       const unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
+      static unsigned long long* d_wave_log = nullptr;  // debug only (RT_DEBUG_PASSES), never freed
+      std::vector<unsigned long long> wave_log;
+      if (debug_passes && count) {
+        if (!d_wave_log) HIPCHK(c, hipMalloc(&d_wave_log, (size_t)trace_grid * 4 * 4 * sizeof(unsigned long long)));
+        wave_log.resize((size_t)trace_grid * 4 * 4);
+      }
       const size_t ovf_group = c->stack_ovf_bytes / sizeof(int2) / (size_t)c->n_groups;
       rtd::WFParams WG[rt_ctx::MAX_GROUPS];
       hipStream_t sg[rt_ctx::MAX_GROUPS];
@@ -762,6 +771,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K.pool_chunk = c->pool_chunk;
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)g * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
+        WP.K.wave_log = (debug_passes && count) ? d_wave_log : nullptr;
         WP.S = c->wfg[g];
         WP.S.pix_xy = c->wf.pix_xy;
         WP.S.pix_acc = c->wf.pix_acc;
@@ -778,15 +788,24 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         for (int g = 1; g < G; g++) HIPCHK(c, hipStreamWaitEvent(sg[g], es, 0));
         c->event_pool.push_back(es);  // reusable once the waits are enqueued
       }
+      // Groups are staggered: group g starts once group g-1 has finished pass `stagger`, so
+      // its busy early passes fill the CUs that group g-1's latency-bound late passes leave idle.
+      const int last_pass = std::max(0, fp->max_bounce);
+      const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
+      hipEvent_t prev_stagger = nullptr, prev_blend = nullptr;
       for (int g = 0; g < G; g++) {
+        rtd::WFParams& WP = WG[g];
+        if (prev_stagger) {
+          HIPCHK(c, hipStreamWaitEvent(sg[g], prev_stagger, 0));
+          c->event_pool.push_back(prev_stagger);  // reusable once the wait is enqueued
+        }
         const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots_g[g] + 255) / 256));
-        HIPCHK(c, hipMemsetAsync(WG[g].S.cnt, 0, 64, sg[g]));
-        hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, sg[g], WG[g]);
+        HIPCHK(c, hipMemsetAsync(WP.S.cnt, 0, 64, sg[g]));
+        WP.pass = 0;
+        hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, sg[g], WP);
         HIPCHK(c, hipGetLastError());
-      }
-      for (int pass = 0; pass <= std::max(0, fp->max_bounce); pass++) {
-        for (int g = 0; g < G; g++) {  // interleaved issue: every stream always has queued work
-          rtd::WFParams& WP = WG[g];
+        prev_stagger = nullptr;
+        for (int pass = 0; pass <= last_pass; pass++) {
           WP.pass = pass;
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
@@ -810,25 +829,51 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
                     "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
                     h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
             HIPCHK(c, hipMemset(c->d_stats + 6, 0, 10 * sizeof(unsigned long long)));
+            if (WP.K.wave_log) {
+              HIPCHK(c, hipMemcpy(wave_log.data(), d_wave_log, wave_log.size() * 8, hipMemcpyDeviceToHost));
+              unsigned long long t0min = ~0ull, t1max = 0, t0max = 0, dmax = 0, itmax = 0, rmax = 0, cmax = 0;
+              std::vector<unsigned long long> ends;
+              double clk_sum = 0.0, wt_sum = 0.0;
+              for (size_t w = 0; w < wave_log.size() / 4; w++) {
+                const unsigned long long* e = &wave_log[4 * w];
+                const unsigned long long its = e[2] & 0xfffffull, cyc = e[2] >> 20;
+                t0min = std::min(t0min, e[0]); t0max = std::max(t0max, e[0]); t1max = std::max(t1max, e[1]);
+                if (e[1] - e[0] > dmax) { dmax = e[1] - e[0]; itmax = its; rmax = e[3]; cmax = cyc; }
+                if (e[1] > e[0]) { clk_sum += (double)cyc; wt_sum += (double)(e[1] - e[0]); }
+                ends.push_back(e[1]);
+              }
+              fprintf(stderr, "[rt]   shader clock: mean over waves %.0f MHz, longest wave %.0f MHz\n",
+                      wt_sum > 0 ? 100.0 * clk_sum / wt_sum : 0.0, dmax ? 100.0 * (double)cmax / (double)dmax : 0.0);
+              std::sort(ends.begin(), ends.end());
+              auto us = [](unsigned long long t) { return t / 100.0; };  // wall_clock64 = 100 MHz
+              fprintf(stderr, "[rt]   waves: start spread %.1f us, span %.1f us; 50%% done at %.1f us, 90%% at %.1f, "
+                      "99%% at %.1f; longest wave %.1f us (%llu iters, %llu rays)\n", us(t0max - t0min),
+                      us(t1max - t0min), us(ends[ends.size() / 2] - t0min), us(ends[ends.size() * 9 / 10] - t0min),
+                      us(ends[ends.size() * 99 / 100] - t0min), us(dmax), itmax, rmax);
+            }
           }
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
           hipLaunchKernelGGL(rtd::wf_shade, dim3(shade_grid), dim3(256), 0, sg[g], WP);
           HIPCHK(c, hipGetLastError());
+          if (g + 1 < G && pass == std::min(c->stagger, last_pass)) {
+            prev_stagger = take_event(c);
+            if (!prev_stagger) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+            HIPCHK(c, hipEventRecord(prev_stagger, sg[g]));
+          }
         }
-      }
-      // progressive blends in frame order: group g after group g-1
-      const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
-      for (int g = 0; g < G; g++) {
-        if (g > 0) {
-          hipEvent_t eb = take_event(c);
-          if (!eb) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
-          HIPCHK(c, hipEventRecord(eb, sg[g - 1]));
-          HIPCHK(c, hipStreamWaitEvent(sg[g], eb, 0));
-          c->event_pool.push_back(eb);
+        // progressive blend in frame order: group g after group g-1
+        if (prev_blend) {
+          HIPCHK(c, hipStreamWaitEvent(sg[g], prev_blend, 0));
+          c->event_pool.push_back(prev_blend);
         }
-        hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WG[g]);
+        hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WP);
         HIPCHK(c, hipGetLastError());
+        if (g + 1 < G) {
+          prev_blend = take_event(c);
+          if (!prev_blend) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+          HIPCHK(c, hipEventRecord(prev_blend, sg[g]));
+        }
       }
       if (G > 1) {  // the caller's stream joins the last group
         hipEvent_t ej = take_event(c);

@@ -421,7 +421,10 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
   unsigned int pool_next = 0, pool_end = 0;
   const unsigned int tail_rays = gridDim.x * TL_LANES * 4u;
-  bool drained = false;
+  // only as many waves as the queue can feed take part: every claim is an atomic on one word,
+  // and thousands of empty-handed claims in a small late pass serialise at that address
+  const unsigned int wave_id = blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6);
+  bool drained = wave_id >= (nq + 63u) / 64u;
   const int lane = (int)(threadIdx.x & 63);
   int entry = 0, parked = 0;
   bool haveParked = false;
@@ -433,6 +436,9 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
   unsigned int ray_steps = 0, ray_steps_max = 0;  // COUNT: node + triangle steps of the lane's ray
   unsigned long long v_itN = 0, v_itT = 0, v_itO = 0, v_park = 0, v_busyO = 0;  // COUNT: lane utilisation
+  unsigned long long v_rays = 0;
+  const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
+  const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
 
   while (true) {
     if (COUNT) v_iter++;
@@ -587,11 +593,19 @@ __global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
     }
     if (busy && finished) {
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
-      if (COUNT) { ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; }
+      if (COUNT) { ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; v_rays++; }
       busy = false;
     }
   }
   if (COUNT) {
+    if (P.wave_log) {
+      unsigned long long r = v_rays;
+      for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+      if ((threadIdx.x & 63) == 0) {
+        unsigned long long* w = P.wave_log + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+        w[0] = t_start; w[1] = wall_clock64(); w[2] = v_iter | ((clock64() - c_start) << 20); w[3] = r;
+      }
+    }
     for (int off = 32; off > 0; off >>= 1) {
       v_int += __shfl_xor(v_int, off);
       v_leaf += __shfl_xor(v_leaf, off);
