@@ -377,20 +377,34 @@ RTD f3 EvalClearcoat(const Mat& mat, f3 V, f3 L, f3 H, float& pdf) {  // RT:986-
   return splat(0.25f) * mat.clearcoat * F * D * G / (4.0f * L.z * V.z);
 }
 
-RTD f3 DisneyEval(const Mat& material, f3 V, f3 N, f3 L, float& bsdfPdf) {  // RT:1002-1067
+// The part of DisneyEval / DisneySample that depends only on (material, V, N): one bounce's
+// NEE evaluation, BSDF sample and continuation evaluation share it (same operations, computed
+// once instead of three times).
+struct BsdfFrame {
+  float eta;
+  f3 T, B, V;  // tangent frame of N (RT:396-407) and V in it
+  f3 specCol, sheenCol;
+};
+RTD BsdfFrame bsdf_frame(const Mat& material, f3 V, f3 N) {
+  BsdfFrame F;
+  F.eta = dot(V, N) > 0.0f ? (1.0f / material.IOR) : material.IOR;  // R10 (RT:1010, RT:1079)
+  getTangent(N, F.T, F.B);
+  F.V = ToLocal(F.T, F.B, N, V);
+  GetSpecColor(material, F.eta, F.specCol, F.sheenCol);
+  return F;
+}
+
+RTD f3 DisneyEval(const BsdfFrame& F, const Mat& material, f3 N, f3 L, float& bsdfPdf) {  // RT:1002-1067
   bsdfPdf = 0.0f;
   f3 f = splat(0.0f);
-  float eta = dot(V, N) > 0.0f ? (1.0f / material.IOR) : material.IOR;  // R10
-  f3 T, B;
-  getTangent(N, T, B);
-  V = ToLocal(T, B, N, V);
+  const float eta = F.eta;
+  const f3 T = F.T, B = F.B, V = F.V;
   L = ToLocal(T, B, N, L);
   f3 H;
   if (L.z > 0.0f) H = normalize(L + V);
   else H = normalize(L + V * eta);
   if (H.z < 0.0f) H = -H;
-  f3 specCol, sheenCol;
-  GetSpecColor(material, eta, specCol, sheenCol);
+  const f3 specCol = F.specCol, sheenCol = F.sheenCol;
   float diffuseWt, specReflectWt, specRefractWt, clearcoatWt;
   float fresnel = DisneyFresnel(material, eta, dot(L, H), dot(V, H));
   CalculateBSDFLobePdfs(material, specCol, fresnel, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
@@ -413,20 +427,20 @@ RTD f3 DisneyEval(const Mat& material, f3 V, f3 N, f3 L, float& bsdfPdf) {  // R
   }
   return f * fabs_(L.z);
 }
+RTD f3 DisneyEval(const Mat& material, f3 V, f3 N, f3 L, float& bsdfPdf) {
+  return DisneyEval(bsdf_frame(material, V, N), material, N, L, bsdfPdf);
+}
 
-RTD f3 DisneySample(float xi_1, float xi_2, float xi_3, const Mat& material, f3 V, f3 N, f3& L, float& pdf,
-                    bool& isRefract) {  // RT:1070-1161
+RTD f3 DisneySample(const BsdfFrame& F, float xi_1, float xi_2, float xi_3, const Mat& material, f3 N, f3& L,
+                    float& pdf, bool& isRefract) {  // RT:1070-1161
   pdf = 0.0f;
   f3 f = splat(0.0f);
   isRefract = false;
   float r1 = xi_1;
   float r2 = xi_2;
-  float eta = dot(V, N) > 0.0f ? (1.0f / material.IOR) : material.IOR;
-  f3 T, B;
-  getTangent(N, T, B);
-  V = ToLocal(T, B, N, V);
-  f3 specCol, sheenCol;
-  GetSpecColor(material, eta, specCol, sheenCol);
+  const float eta = F.eta;
+  const f3 T = F.T, B = F.B, V = F.V;
+  const f3 specCol = F.specCol, sheenCol = F.sheenCol;
   float diffuseWt, specReflectWt, specRefractWt, clearcoatWt;
   float approxFresnel = DisneyFresnel(material, eta, V.z, V.z);
   CalculateBSDFLobePdfs(material, specCol, approxFresnel, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
@@ -466,6 +480,10 @@ RTD f3 DisneySample(float xi_1, float xi_2, float xi_3, const Mat& material, f3 
   }
   L = ToWorld(T, B, N, L);
   return f * fabs_(dot(N, L));
+}
+RTD f3 DisneySample(float xi_1, float xi_2, float xi_3, const Mat& material, f3 V, f3 N, f3& L, float& pdf,
+                    bool& isRefract) {
+  return DisneySample(bsdf_frame(material, V, N), xi_1, xi_2, xi_3, material, N, L, pdf, isRefract);
 }
 
 // ----------------------------------------------------------- BRDF mode (enableBSDF == false)
