@@ -60,7 +60,7 @@ struct rt_ctx {
   double kernel_ms = 0.0, trace_ms = 0.0;
   uint64_t launches = 0, trace_launches = 0;
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
-  int trace_bpc = 0;                          // wavefront traversal kernel
+  int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
@@ -246,21 +246,40 @@ int occupancy(rt_ctx* c) {
   c->trace_mode = rtd::TM_DUAL;
   if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode0 = c->trace_mode = std::max(0, std::min(3, atoi(e)));
   if (const char* e = getenv("RT_TRACE_MODE0")) c->trace_mode0 = std::max(0, std::min(3, atoi(e)));
-  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256,
-                                                         c->trace_lds));
-  c->trace_bpc = std::max(1, bpc);
-  if (const char* e = getenv("RT_TRACE_BPC")) c->trace_bpc = std::max(1, atoi(e));
+  // persistent grids: as many blocks as can be resident, per schedule (their register counts differ)
+  auto occ = [&](int mode) {
+    int b = 0;
+    hipError_t e;
+    switch (mode) {
+      case rtd::TM_IFIF:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true>, 256, c->trace_lds);
+        break;
+      case rtd::TM_WW:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true>, 256, c->trace_lds);
+        break;
+      case rtd::TM_DUAL:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true>, 256, c->trace_lds);
+        break;
+      default:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256, c->trace_lds);
+    }
+    return e == hipSuccess ? std::max(1, b) : 1;
+  };
+  c->trace_bpc0 = occ(c->trace_mode0);
+  c->trace_bpc = occ(c->trace_mode);
+  bpc = c->trace_bpc;
+  if (const char* e = getenv("RT_TRACE_BPC")) c->trace_bpc0 = c->trace_bpc = std::max(1, atoi(e));
   if (const char* e = getenv("RT_POOL_CHUNK")) c->pool_chunk = std::max(64, atoi(e) / 64 * 64);
   if (getenv("RT_DEBUG")) {
-    fprintf(stderr, "[rt] trace: lds entries %d (%d B/block), occupancy API %d blocks/CU, using %d; megakernel %d\n",
-            kl, c->trace_lds, bpc, c->trace_bpc, c->blocks_per_cu);
+    fprintf(stderr, "[rt] trace: lds entries %d (%d B/block), occupancy API %d blocks/CU, using %d (pass 0: %d); "
+            "megakernel %d\n", kl, c->trace_lds, bpc, c->trace_bpc, c->trace_bpc0, c->blocks_per_cu);
     for (int l = 0; l <= 40960; l += 8192) {
       int b = 0;
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256, l);
       fprintf(stderr, "[rt]   occupancy(lds=%d) = %d\n", l, b);
     }
   }
-  const size_t lanes = (size_t)c->n_cus * c->trace_bpc * 256;
+  const size_t lanes = (size_t)c->n_cus * std::max(c->trace_bpc, c->trace_bpc0) * 256;
   const int entries = std::max(c->stack_entries, c->qstack_entries);
   const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2) * c->n_groups;
   if (need > c->stack_ovf_bytes) {
@@ -746,7 +765,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       // split the batch into frame groups (frames [f0, f1) each), one stream per group
       const int G = std::min(c->n_groups, nf);
       static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
-      const unsigned int trace_grid = (unsigned)(c->n_cus * c->trace_bpc);
+      const unsigned int trace_grid = (unsigned)(c->n_cus * std::max(c->trace_bpc, c->trace_bpc0));
+      const unsigned int trace_grid0 = (unsigned)(c->n_cus * c->trace_bpc0);
+      const unsigned int trace_grid1 = (unsigned)(c->n_cus * c->trace_bpc);
       static unsigned long long* d_wave_log = nullptr;  // debug only (RT_DEBUG_PASSES), never freed
       std::vector<unsigned long long> wave_log;
       if (debug_passes && count) {
@@ -810,7 +831,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));
-          launch_trace(c, count, dim3(trace_grid), WP, sg[g]);
+          launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g]);
           HIPCHK(c, hipGetLastError());
           HIPCHK(c, hipEventRecord(t1, sg[g]));
           c->trace_events.push_back({t0, t1});

@@ -387,8 +387,11 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   L.haveCur = r[0] != Q_EMPTY || tl_pop(L, S, cull);
 }
 
+#ifndef RT_TRACE_WPE
+#define RT_TRACE_WPE 1
+#endif
 template <bool COUNT, int MODE, bool WIDE>
-__global__ __launch_bounds__(256) void wf_trace(const WFParams W) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE))) void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
