@@ -3,8 +3,11 @@
 
 Workload (default): config C3 = floor + loong_100000 (copper), 1920x1080, maxBounce 8,
 HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs.py).
-One *step* = ``--frames-per-step`` progressive frames (1 spp each) of the whole frame,
-rendered by one kernel launch per rank over that rank's pixel tiles, followed by the
+One *step* = ``--frames-per-step`` (default 512) progressive frames (1 spp each) of the whole
+frame, rendered by one rt_render call per rank over that rank's pixel tiles (frames in flight
+bounded by the 160M-slot path-state budget: 64 at a time on one GPU, all 512 at once on each of
+8 tile-sharded GPUs, so every rank keeps the same work in flight: strong scaling of a fixed
+frame budget without a per-rank latency floor penalty), followed by the
 frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
 torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
 
@@ -44,7 +47,7 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--frames-per-step", type=int, default=64)
+    ap.add_argument("--frames-per-step", type=int, default=512)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)

@@ -49,7 +49,9 @@ enum {
   RT_ERR_LIMIT = -6     /* scene exceeds a kernel limit (leaf > 16 tris, depth > 64) */
 };
 
-enum { RT_MAX_FRAMES_PER_LAUNCH = 64 };
+/* Frames per kernel batch; the path-state budget (216 B per pixel-frame, RT_MAX_SLOTS, default
+ * 160M) bounds it too: 64 frames at 1920x1080 on one GPU, 512 on each of 8 tile-sharded GPUs. */
+enum { RT_MAX_FRAMES_PER_LAUNCH = 1024 };
 
 /* Disney material (src/core/Material.h:25-46), 24 floats, same layout as rts_material. */
 typedef struct rt_material {

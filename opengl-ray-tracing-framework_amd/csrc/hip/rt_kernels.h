@@ -33,8 +33,8 @@ struct KParams {
   int enable_mis, enable_env, enable_bsdf;
   float env_intensity, env_angle;
   int max_bounce, flags, n_frames;
-  int loop_num[RT_MAX_FRAMES_PER_LAUNCH];
-  float rand_origin[RT_MAX_FRAMES_PER_LAUNCH];
+  const int* __restrict__ loop_num;       // per frame of this launch (device table)
+  const float* __restrict__ rand_origin;  // per frame of this launch (device table)
   int W, H, tile_w, tile_h, tiles_x, rank, world;
   unsigned int n_work;
   const GNode* __restrict__ nodes;  // binary tree; GNode.ref.z = DFS rank of the first leaf on the right

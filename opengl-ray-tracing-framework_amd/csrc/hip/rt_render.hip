@@ -62,6 +62,11 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
+  // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table
+  int* h_ftab = nullptr;                      // [cap] loop_num then [cap] rand_origin bits
+  int* d_ftab = nullptr;
+  size_t ftab_cap = 0;
+  hipEvent_t ftab_event = nullptr;            // the last upload (the host table is reused after it)
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
   int pool_chunk = 256;                       // rays per queue atomic in wf_trace
@@ -400,6 +405,9 @@ int rt_destroy(rt_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   for (auto& a : c->aux) if (a) (void)hipStreamDestroy(a);
+  if (c->ftab_event) (void)hipEventDestroy(c->ftab_event);
+  if (c->h_ftab) (void)hipHostFree(c->h_ftab);
+  dfree(c->d_ftab);
   dfree(c->d_pix);
   dfree(c->d_stack_ovf);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -715,23 +723,45 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     for (int g = 1; g < c->n_groups; g++)
       if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
   }
+  // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12).
+  // The traced frames' (loopNum, randOrigin) go to a device table in one upload.
+  if (n_frames > 0 && (size_t)n_frames > c->ftab_cap) {
+    if (c->ftab_event) HIPCHK(c, hipEventSynchronize(c->ftab_event));
+    if (c->h_ftab) (void)hipHostFree(c->h_ftab);
+    c->h_ftab = nullptr;
+    dfree(c->d_ftab);
+    const size_t cap = std::max<size_t>(1024, (size_t)n_frames);
+    HIPCHK(c, hipHostMalloc((void**)&c->h_ftab, 2 * cap * sizeof(int)));
+    HIPCHK(c, hipMalloc((void**)&c->d_ftab, 2 * cap * sizeof(int)));
+    c->ftab_cap = cap;
+  }
+  if (!c->ftab_event) HIPCHK(c, hipEventCreateWithFlags(&c->ftab_event, hipEventDisableTiming));
+  HIPCHK(c, hipEventSynchronize(c->ftab_event));  // the previous call's upload has read h_ftab
+  int n_traced = 0;
+  for (int k = 0; k < n_frames; k++) {
+    if (fp->max_iterations == -1 || c->loop_num < fp->max_iterations) c->loop_num++;
+    if (!(fp->max_iterations == -1 || c->loop_num < fp->max_iterations)) continue;
+    c->h_ftab[n_traced] = c->loop_num;
+    memcpy(&c->h_ftab[c->ftab_cap + n_traced], &rand_origin[k], 4);
+    n_traced++;
+  }
+  if (n_traced > 0) {
+    HIPCHK(c, hipMemcpyAsync(c->d_ftab, c->h_ftab, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ftab + c->ftab_cap, c->h_ftab + c->ftab_cap, (size_t)n_traced * sizeof(int),
+                             hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(c, hipEventRecord(c->ftab_event, c->stream));
+  const int* d_loop = c->d_ftab;
+  const float* d_ro = reinterpret_cast<const float*>(c->d_ftab + c->ftab_cap);
   int done = 0;
-  while (done < n_frames) {
+  while (done < n_traced) {
     KParams P;
     memset(&P, 0, sizeof(P));
-    int nf = 0;
-    // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12)
     const int cap = (fp->flags & RT_FLAG_MEGAKERNEL) ? RT_MAX_FRAMES_PER_LAUNCH : c->frames_cap;
-    while (done < n_frames && nf < cap) {
-      if (fp->max_iterations == -1 || c->loop_num < fp->max_iterations) c->loop_num++;
-      bool traced = fp->max_iterations == -1 || c->loop_num < fp->max_iterations;
-      done++;
-      if (!traced) continue;
-      P.loop_num[nf] = c->loop_num;
-      P.rand_origin[nf] = rand_origin[done - 1];
-      nf++;
-    }
-    if (nf == 0) continue;
+    const int nf = std::min(cap, n_traced - done);
+    P.loop_num = d_loop + done;
+    P.rand_origin = d_ro + done;
+    done += nf;
     memcpy(P.pos, fp->position, 12); memcpy(P.lbc, fp->left_bottom_corner, 12);
     memcpy(P.right, fp->right, 12); memcpy(P.up, fp->up, 12);
     P.half_w = fp->half_w; P.half_h = fp->half_h;
@@ -782,10 +812,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         const int f0 = g * nf / G, f1 = (g + 1) * nf / G;
         rtd::WFParams& WP = WG[g];
         WP.K = P;
-        for (int f = f0; f < f1; f++) {
-          WP.K.loop_num[f - f0] = P.loop_num[f];
-          WP.K.rand_origin[f - f0] = P.rand_origin[f];
-        }
+        WP.K.loop_num = P.loop_num + f0;
+        WP.K.rand_origin = P.rand_origin + f0;
         WP.K.n_frames = f1 - f0;
         WP.K.n_work = (unsigned)c->n_valid;
         WP.K.lds_entries = c->trace_lds_entries;

@@ -18,7 +18,7 @@ import numpy as np
 from ._paths import lib_path
 
 RT_OK, RT_ERR_ARG, RT_ERR_HIP, RT_ERR_STATE, RT_ERR_NOMEM, RT_ERR_NODEVICE, RT_ERR_LIMIT = 0, -1, -2, -3, -4, -5, -6
-RT_MAX_FRAMES_PER_LAUNCH = 64
+RT_MAX_FRAMES_PER_LAUNCH = 1024
 RT_FLAG_NO_CULL = 1
 RT_FLAG_COUNT_VISITS = 2
 RT_FLAG_MEGAKERNEL = 4

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the committed fixtures under tests/golden/ (run in the build container).
 
-* rand_origins.json   randOrigin_k for k = 1..4096 (glibc srand(20221002), main.cpp:190)
+* rand_origins.json   randOrigin_k for k = 1..16384 (glibc srand(20221002), main.cpp:190)
 * hdr_ref.json        the reference HDRLoader's decode of peppermint_powerplant_1k.hdr, from
                       oracle/_ref/ref_hdr_dump (thirdparty/hdrloader/hdrloader.cpp compiled from
                       its own sources by oracle/Makefile): size, checksums, sampled texels
@@ -40,9 +40,9 @@ def read_ref_dump(path: Path):
 
 def main() -> int:
     GOLD.mkdir(parents=True, exist_ok=True)
-    ro = sl.cpu_rand_origins(cf.RAND_SEED, 4096)
+    ro = sl.cpu_rand_origins(cf.RAND_SEED, 16384)
     (GOLD / "rand_origins.json").write_text(json.dumps({
-        "note": "randOrigin_k = 674764*(rand()/(RAND_MAX+1.0)+1) after glibc srand(20221002), k=1..4096 "
+        "note": "randOrigin_k = 674764*(rand()/(RAND_MAX+1.0)+1) after glibc srand(20221002), k=1..16384 "
                 "(main.cpp:190, src/core/Utility.h:11-17); float32 bit patterns",
         "seed": cf.RAND_SEED, "bits": [int(x) for x in ro.view(np.uint32)]}))
 
