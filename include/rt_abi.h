@@ -163,6 +163,17 @@ int rt_copy_accum_device(rt_ctx* ctx, void* dst_device, size_t bytes);
  * this ctx's device into a width*height*3 float frame (device pointer). */
 int rt_assemble_frame(rt_ctx* ctx, const void* gathered_device, int32_t world, void* frame_device);
 
+/* Display / screenshot — replaces the tone-mapping pass
+ * (src/shaders/fragment_shader_tone_mapping.glsl:66-93, main.cpp:215-227) or the screen blit
+ * (fragment_shader_screen.glsl:6-9) plus the 8-bit read-back of SaveFrame (Utility.h:19-30).
+ * flags: RT_DISPLAY_TONEMAP (enableToneMapping: simpleACES), RT_DISPLAY_GAMMA
+ * (enableGammaCorrection: pow(c, 1/2.2), only with TONEMAP, as in main.cpp:216).
+ * frame_device: an assembled width*height*3 float frame (rt_assemble_frame), or NULL for this
+ * context's own accumulation (single rank only).  rgb8_host: width*height*3 bytes, row 0 = top
+ * (PNG order).  Synchronous. */
+enum { RT_DISPLAY_TONEMAP = 1, RT_DISPLAY_GAMMA = 2 };
+int rt_tonemap(rt_ctx* ctx, const float* frame_device, int32_t flags, uint8_t* rgb8_host);
+
 #ifdef __cplusplus
 }
 #endif

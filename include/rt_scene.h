@@ -116,6 +116,10 @@ int rts_camera(float yaw_deg, float pitch_deg, float zoom_deg, float screen_rati
 /* randOrigin_k = 674764 * (rand()/(RAND_MAX+1.0) + 1) after srand(seed), glibc rand. */
 int rts_cpu_rand_origins(unsigned int seed, int n, float* out);
 
+/* 8-bit RGB PNG (stbi_write_png in SaveFrame, src/core/Utility.h:19-30): width*height*3 bytes,
+ * row 0 = top (rt_tonemap's output order).  Stored (uncompressed) deflate, no zlib needed. */
+int rts_write_png(const char* path, int width, int height, const uint8_t* rgb);
+
 #ifdef __cplusplus
 }
 #endif

@@ -447,4 +447,46 @@ __global__ __launch_bounds__(256) void rt_set_material_kernel(float4* __restrict
   if (i < count) trin[3 * (size_t)(first + i)].w = __int_as_float(id);
 }
 
+// ------------------------------------------------------------ display (rt_tonemap)
+// fragment_shader_tone_mapping.glsl:66-93 (simpleACES + pow 1/2.2) or the screen blit,
+// GL unorm8 conversion, SaveFrame's vertical flip (out row 0 = top).  Reads either this
+// rank's tile accumulation (world == 1) or an assembled H x W x 3 frame (row 0 = bottom).
+RTD f3 simple_aces(f3 c) {  // TM:66-75
+  const float a = 2.51f, b = 0.03f, y = 2.43f, d = 0.59f, e = 0.14f;
+  const f3 num = c * (a * c + splat(b));
+  const f3 den = c * (y * c + splat(d)) + splat(e);
+  const f3 r = num / den;
+  return mk3(clamp_(r.x, 0.0f, 1.0f), clamp_(r.y, 0.0f, 1.0f), clamp_(r.z, 0.0f, 1.0f));
+}
+RTD unsigned char unorm8(float f) { return (unsigned char)(int)(clamp_(f, 0.0f, 1.0f) * 255.0f + 0.5f); }
+
+__global__ __launch_bounds__(256) void rt_display_kernel(const float4* __restrict__ tiles, const float* __restrict__ frame,
+                                                         unsigned char* __restrict__ out, int W, int H, int tile_w,
+                                                         int tile_h, int tiles_x, int flags) {
+  const int px = blockIdx.x * blockDim.x + threadIdx.x, py = blockIdx.y;
+  if (px >= W || py >= H) return;
+  f3 c;
+  if (tiles) {
+    const int tx = px / tile_w, ty = py / tile_h;
+    const size_t idx = (size_t)(ty * tiles_x + tx) * (size_t)(tile_w * tile_h) +
+                       (size_t)(py - ty * tile_h) * tile_w + (px - tx * tile_w);
+    const float4 v = tiles[idx];
+    c = mk3(v.x, v.y, v.z);
+  } else {
+    const float* p = frame + 3 * ((size_t)py * W + px);
+    c = mk3(p[0], p[1], p[2]);
+  }
+  if (flags & 1) {
+    c = simple_aces(c);
+    if (flags & 2) {
+      const float g = 1.0f / 2.2f;
+      c = mk3(pow_(c.x, g), pow_(c.y, g), pow_(c.z, g));
+    }
+  }
+  unsigned char* o = out + 3 * ((size_t)(H - 1 - py) * W + px);
+  o[0] = unorm8(c.x);
+  o[1] = unorm8(c.y);
+  o[2] = unorm8(c.z);
+}
+
 }  // namespace rtd

@@ -72,6 +72,8 @@ struct rt_ctx {
   int pool_chunk = 256;                       // rays per queue atomic in wf_trace
   int stagger = -1;                           // >= 0: group g starts after group g-1's pass `stagger` (measured slower)
   int2* d_stack_ovf = nullptr;
+  void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
+  size_t disp_bytes = 0;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
   void* wf_mem = nullptr;
@@ -410,6 +412,7 @@ int rt_destroy(rt_ctx* c) {
   dfree(c->d_ftab);
   dfree(c->d_pix);
   dfree(c->d_stack_ovf);
+  dfree(c->d_disp);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -994,6 +997,28 @@ int rt_render(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, in
   int rc = rt_render_async(c, fp, rand_origin, n_frames);
   if (rc) return rc;
   return st ? rt_stats_get(c, st) : rt_synchronize(c);
+}
+
+int rt_tonemap(rt_ctx* c, const float* frame_device, int32_t flags, uint8_t* rgb8_host) {
+  if (!c || !rgb8_host) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "resize first");
+  if (!frame_device && c->world != 1)
+    return fail(c, RT_ERR_STATE, "a multi-rank context displays an assembled frame (rt_assemble_frame)");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t bytes = (size_t)c->W * c->H * 3;
+  if (bytes > c->disp_bytes) {
+    dfree(c->d_disp);
+    HIPCHK(c, hipMalloc(&c->d_disp, bytes));
+    c->disp_bytes = bytes;
+  }
+  dim3 grid((c->W + 255) / 256, c->H);
+  hipLaunchKernelGGL(rtd::rt_display_kernel, grid, dim3(256), 0, c->stream,
+                     frame_device ? nullptr : c->d_accum, frame_device, (unsigned char*)c->d_disp, c->W, c->H,
+                     c->tile_w, c->tile_h, c->tiles_x, (int)flags);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(rgb8_host, c->d_disp, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
 }
 
 int rt_get_stream(const rt_ctx* c, void** stream) {

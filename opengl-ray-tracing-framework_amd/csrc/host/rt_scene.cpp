@@ -854,7 +854,7 @@ struct Reader {
     return d[pos++];
   }
 };
-bool old_decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:161-190
+static bool old_decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:161-190
   int rshift = 0;
   while (len > 0) {
     scan[0][0] = (unsigned char)f.getc();
@@ -877,7 +877,7 @@ bool old_decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:161-1
   }
   return true;
 }
-bool decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:118-159
+static bool decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:118-159
   if (len < 8 || len > 0x7fff) return old_decrunch(scan, len, f);
   int i = f.getc();
   if (i != 2) {
@@ -907,7 +907,7 @@ bool decrunch(unsigned char (*scan)[4], int len, Reader& f) {  // HDRL:118-159
   }
   return !f.eof;
 }
-float convert_component(int expo, int val) {  // HDRL:99-104
+static float convert_component(int expo, int val) {  // HDRL:99-104
   float v = (float)val / 256.0f;
   float d = (float)pow(2.0, (double)expo);
   return v * d;
@@ -1030,6 +1030,79 @@ int rts_camera(float yaw_deg, float pitch_deg, float zoom_deg, float screen_rati
   out[13] = halfW;
   out[14] = out[15] = out[16] = 0.0f;
   return RTS_OK;
+}
+
+// ------------------------------------------------------------------------------ PNG
+// (static, distinct names: inside extern "C" a helper called crc32 would be the global C symbol
+// and bind to zlib's crc32 in processes that load zlib)
+static uint32_t png_crc_table[256];
+static bool png_crc_ready = false;
+static uint32_t png_crc32(const unsigned char* d, size_t n, uint32_t c = 0xffffffffu) {
+  if (!png_crc_ready) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t v = i;
+      for (int k = 0; k < 8; k++) v = (v & 1u) ? 0xedb88320u ^ (v >> 1) : v >> 1;
+      png_crc_table[i] = v;
+    }
+    png_crc_ready = true;
+  }
+  for (size_t i = 0; i < n; i++) c = png_crc_table[(c ^ d[i]) & 0xffu] ^ (c >> 8);
+  return c;
+}
+static void png_put32(std::vector<unsigned char>& v, uint32_t x) {
+  v.push_back((unsigned char)(x >> 24)); v.push_back((unsigned char)(x >> 16));
+  v.push_back((unsigned char)(x >> 8)); v.push_back((unsigned char)x);
+}
+static void png_chunk(FILE* f, const char* type, const std::vector<unsigned char>& data) {
+  std::vector<unsigned char> b;
+  png_put32(b, (uint32_t)data.size());
+  b.insert(b.end(), type, type + 4);
+  b.insert(b.end(), data.begin(), data.end());
+  const uint32_t c = png_crc32(b.data() + 4, b.size() - 4) ^ 0xffffffffu;
+  png_put32(b, c);
+  fwrite(b.data(), 1, b.size(), f);
+}
+int rts_write_png(const char* path, int width, int height, const uint8_t* rgb) {
+  if (!path || !rgb || width <= 0 || height <= 0) return RTS_ERR_ARG;
+  FILE* f = fopen(path, "wb");
+  if (!f) return RTS_ERR_IO;
+  static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  fwrite(sig, 1, 8, f);
+  std::vector<unsigned char> ihdr;
+  png_put32(ihdr, (uint32_t)width);
+  png_put32(ihdr, (uint32_t)height);
+  const unsigned char rest[5] = {8, 2, 0, 0, 0};  // 8-bit, RGB, deflate, filter 0, no interlace
+  ihdr.insert(ihdr.end(), rest, rest + 5);
+  png_chunk(f, "IHDR", ihdr);
+  // zlib stream of stored deflate blocks over the filtered scanlines (filter byte 0)
+  const size_t row = (size_t)width * 3 + 1, raw = row * (size_t)height;
+  std::vector<unsigned char> z;
+  z.reserve(raw + raw / 65535 * 5 + 16);
+  z.push_back(0x78);
+  z.push_back(0x01);
+  uint32_t s1 = 1, s2 = 0;  // Adler-32
+  size_t pos = 0;
+  std::vector<unsigned char> block;
+  while (pos < raw) {
+    const size_t n = std::min<size_t>(65535, raw - pos);
+    z.push_back(pos + n == raw ? 1 : 0);
+    z.push_back((unsigned char)(n & 0xff)); z.push_back((unsigned char)(n >> 8));
+    z.push_back((unsigned char)(~n & 0xff)); z.push_back((unsigned char)((~n >> 8) & 0xff));
+    for (size_t k = pos; k < pos + n; k++) {
+      const size_t y = k / row, x = k % row;
+      const unsigned char b = x == 0 ? 0 : rgb[y * (size_t)width * 3 + (x - 1)];
+      z.push_back(b);
+      s1 = (s1 + b) % 65521u;
+      s2 = (s2 + s1) % 65521u;
+    }
+    pos += n;
+  }
+  png_put32(z, (s2 << 16) | s1);
+  png_chunk(f, "IDAT", z);
+  png_chunk(f, "IEND", std::vector<unsigned char>());
+  const bool ok = fflush(f) == 0;
+  fclose(f);
+  return ok ? RTS_OK : RTS_ERR_IO;
 }
 
 int rts_cpu_rand_origins(unsigned int seed, int n, float* out) {

@@ -33,8 +33,9 @@ ABI_SYMBOLS = (
     "rt_update_materials", "rt_set_env", "rt_resize", "rt_reset", "rt_set_loop_num", "rt_get_loop_num",
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
-    "rt_assemble_frame",
+    "rt_assemble_frame", "rt_tonemap",
 )
+RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
 
 class RtMaterial(C.Structure):
@@ -159,6 +160,7 @@ def lib() -> C.CDLL:
         L.rt_accum_device.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), _i32p, _i32p]
         L.rt_copy_accum_device.argtypes = [vp, vp, C.c_size_t]
         L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
+        L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
 
@@ -329,3 +331,11 @@ class Renderer:
     def assemble_frame(self, gathered_ptr: int, world: int, frame_ptr: int) -> None:
         self._check(self._L.rt_assemble_frame(self._h, C.c_void_p(gathered_ptr), world, C.c_void_p(frame_ptr)),
                     "rt_assemble_frame")
+
+    def tonemap(self, flags: int = RT_DISPLAY_TONEMAP | RT_DISPLAY_GAMMA, frame_ptr: Optional[int] = None) -> np.ndarray:
+        """The displayed 8-bit image (H, W, 3), row 0 = top: the tone-mapping pass / screen blit +
+        SaveFrame's read-back (rt_abi.h rt_tonemap); frame_ptr = an assembled device frame."""
+        out = np.zeros((self.height, self.width, 3), np.uint8)
+        self._check(self._L.rt_tonemap(self._h, C.c_void_p(frame_ptr) if frame_ptr else None, int(flags),
+                                       out.ctypes.data_as(C.POINTER(C.c_uint8))), "rt_tonemap")
+        return out

@@ -111,6 +111,7 @@ def lib() -> C.CDLL:
         L.rts_free.restype = None
         L.rts_camera.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, _f32p]
         L.rts_cpu_rand_origins.argtypes = [C.c_uint, C.c_int, _f32p]
+        L.rts_write_png.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
 
@@ -303,3 +304,12 @@ def cpu_rand_origins(seed: int, n: int) -> np.ndarray:
     out = np.zeros(n, np.float32)
     _check(lib().rts_cpu_rand_origins(seed, n, _fp(out)), "rts_cpu_rand_origins")
     return out
+
+
+def write_png(path: str, rgb: np.ndarray) -> None:
+    """8-bit RGB (H, W, 3), row 0 = top -> PNG (rts_write_png, SaveFrame's stbi_write_png)."""
+    a = np.ascontiguousarray(rgb, np.uint8)
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError("expected an (H, W, 3) uint8 image")
+    _check(lib().rts_write_png(str(path).encode(), a.shape[1], a.shape[0], a.ctypes.data_as(C.POINTER(C.c_uint8))),
+           "rts_write_png")

@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
         L.orc_to_spherical.argtypes = [_f32p, C.c_float, _f32p]
         L.orc_disney_eval.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_disney_sample.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, C.POINTER(C.c_int)]
+        L.orc_display.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
 
@@ -124,3 +125,12 @@ def render(scene: OracleScene, frames: Sequence[dict], W: int, H: int, x0: int =
     if rc != 0:
         raise RuntimeError(f"orc_render failed: {rc}")
     return acc, cnt.as_dict()
+
+
+def display(frame: np.ndarray, flags: int = 3) -> np.ndarray:
+    """Tone map / blit + 8-bit conversion + SaveFrame flip of an (H, W, 3) float frame (row 0 =
+    bottom) -> (H, W, 3) uint8, row 0 = top (TM:66-93, Utility.h:19-30)."""
+    f = np.ascontiguousarray(frame, np.float32)
+    out = np.zeros(f.shape, np.uint8)
+    lib().orc_display(f.ctypes.data_as(_f32p), f.shape[1], f.shape[0], int(flags), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out

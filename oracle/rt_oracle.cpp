@@ -1137,4 +1137,39 @@ void orc_disney_sample(const float* mat_texels, const float* xi, const float* V,
   f_out[0] = f.x; f_out[1] = f.y; f_out[2] = f.z; *pdf_out = pdf; *is_refract = refr ? 1 : 0;
 }
 
+
+// ------------------------------------------------------------------ display
+// The presented image: with enableToneMapping the tone-mapping pass (TM:77-93: simpleACES
+// TM:66-75, then pow(c, 1/2.2) with enableGammaCorrection), otherwise the screen blit
+// (fragment_shader_screen.glsl:6-9); written to the 8-bit default framebuffer (GL unorm
+// conversion round(clamp(c, 0, 1) * 255)) and saved by SaveFrame (Utility.h:19-30), which reads
+// rows bottom-up and flips them, so out row 0 is the top of the image.
+// frame: H x W x 3 floats, row 0 = bottom (the accumulation texture); flags: 1 tone map, 2 gamma.
+static vec3 simpleACES(vec3 c) {  // TM:66-75
+  const float a = 2.51f, b = 0.03f, y = 2.43f, d = 0.59f, e = 0.14f;
+  vec3 num = c * (a * c + vec3(b));
+  vec3 den = c * (y * c + vec3(d)) + vec3(e);
+  vec3 r = num / den;
+  return vec3(clamp_(r.x, 0.0f, 1.0f), clamp_(r.y, 0.0f, 1.0f), clamp_(r.z, 0.0f, 1.0f));
+}
+static uint8_t unorm8(float f) {
+  f = clamp_(f, 0.0f, 1.0f);  // NaN -> 0 (fminf/fmaxf)
+  return (uint8_t)(int)(f * 255.0f + 0.5f);
+}
+void orc_display(const float* frame, int W, int H, int flags, uint8_t* out) {
+  for (int py = 0; py < H; py++)
+    for (int px = 0; px < W; px++) {
+      const float* p = frame + 3 * ((size_t)py * W + px);
+      vec3 c(p[0], p[1], p[2]);
+      if (flags & 1) {
+        c = simpleACES(c);
+        if (flags & 2) {
+          const float g = 1.0f / 2.2f;
+          c = vec3(pow_(c.x, g), pow_(c.y, g), pow_(c.z, g));
+        }
+      }
+      uint8_t* o = out + 3 * ((size_t)(H - 1 - py) * W + px);
+      o[0] = unorm8(c.x); o[1] = unorm8(c.y); o[2] = unorm8(c.z);
+    }
+}
 }  // extern "C"
