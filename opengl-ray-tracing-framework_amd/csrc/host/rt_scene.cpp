@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -537,6 +538,142 @@ int build_sah(std::vector<Tri>& tris, std::vector<Node>& nodes, int l, int r, in
   return id;
 }
 
+// The same build, faster and with identical output ("faithful" mode):
+// * the per-axis std::sort runs on a 4-byte index permutation compared through precomputed
+//   centroids (the same (p1+p2+p3)/3 fp32 values); libstdc++'s introsort does the same
+//   comparisons and moves whatever the element type, so the permutation is identical;
+// * prefix/suffix boxes read precomputed per-triangle bounds (the same min3/max3 values);
+// * subtrees over disjoint triangle ranges are built concurrently into local node vectors and
+//   spliced back in the reference's pre-order numbering.
+struct FastBuild {
+  std::vector<float> c[3];      // centroid per triangle and axis
+  std::vector<v3> tmin, tmax;   // per-triangle bounds
+  std::vector<int32_t> perm;    // current triangle order (indices into the input array)
+  int n;
+  int par_depth;
+};
+
+void fast_sort(FastBuild& B, int l, int r, int axis) {
+  const float* key = B.c[axis].data();
+  std::sort(B.perm.data() + l, B.perm.data() + r + 1, [key](int32_t a, int32_t b) { return key[a] < key[b]; });
+}
+
+// appends the subtree over [l, r] to `nodes` in pre-order (local ids); returns its root id
+int fast_sah(FastBuild& B, std::vector<Node>& nodes, int l, int r, int depth) {
+  if (l > r) return 0;
+  nodes.push_back(Node());
+  const int id = (int)nodes.size() - 1;
+  Node nd;
+  nd.left = nd.right = nd.n = nd.index = 0;
+  nd.AA = mk(1145141919.0f, 1145141919.0f, 1145141919.0f);
+  nd.BB = mk(-1145141919.0f, -1145141919.0f, -1145141919.0f);
+  for (int i = l; i <= r; i++) {
+    const int t = B.perm[i];
+    nd.AA.x = gmin(nd.AA.x, B.tmin[t].x); nd.AA.y = gmin(nd.AA.y, B.tmin[t].y); nd.AA.z = gmin(nd.AA.z, B.tmin[t].z);
+    nd.BB.x = gmax(nd.BB.x, B.tmax[t].x); nd.BB.y = gmax(nd.BB.y, B.tmax[t].y); nd.BB.z = gmax(nd.BB.z, B.tmax[t].z);
+  }
+  if ((r - l + 1) <= B.n) {
+    nd.n = r - l + 1;
+    nd.index = l;
+    nodes[id] = nd;
+    return id;
+  }
+  float Cost = kINF;
+  int Axis = 0, Split = (l + r) / 2;
+  const int cnt = r - l + 1;
+  std::vector<v3> leftMax(cnt), leftMin(cnt), rightMax(cnt), rightMin(cnt);
+  for (int axis = 0; axis < 3; axis++) {
+    fast_sort(B, l, r, axis);
+    for (int i = l; i <= r; i++) {  // BVH.h:158-168 (the kINF initialisers are overwritten)
+      const int t = B.perm[i];
+      const int k = i - l, kp = (i == l) ? k : k - 1;
+      const v3 pmax = (i == l) ? mk(-kINF, -kINF, -kINF) : leftMax[kp], pmin = (i == l) ? mk(kINF, kINF, kINF) : leftMin[kp];
+      leftMax[k] = mk(gmax(pmax.x, B.tmax[t].x), gmax(pmax.y, B.tmax[t].y), gmax(pmax.z, B.tmax[t].z));
+      leftMin[k] = mk(gmin(pmin.x, B.tmin[t].x), gmin(pmin.y, B.tmin[t].y), gmin(pmin.z, B.tmin[t].z));
+    }
+    for (int i = r; i >= l; i--) {
+      const int t = B.perm[i];
+      const int k = i - l, kp = (i == r) ? k : k + 1;
+      const v3 pmax = (i == r) ? mk(-kINF, -kINF, -kINF) : rightMax[kp], pmin = (i == r) ? mk(kINF, kINF, kINF) : rightMin[kp];
+      rightMax[k] = mk(gmax(pmax.x, B.tmax[t].x), gmax(pmax.y, B.tmax[t].y), gmax(pmax.z, B.tmax[t].z));
+      rightMin[k] = mk(gmin(pmin.x, B.tmin[t].x), gmin(pmin.y, B.tmin[t].y), gmin(pmin.z, B.tmin[t].z));
+    }
+    float cost = kINF;
+    int split = l;
+    for (int i = l; i <= r - 1; i++) {
+      const v3 leftAA = leftMin[i - l], leftBB = leftMax[i - l];
+      float lenx = leftBB.x - leftAA.x, leny = leftBB.y - leftAA.y, lenz = leftBB.z - leftAA.z;
+      const float leftS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
+      const float leftCost = leftS * (float)(i - l + 1);
+      const v3 rightAA = rightMin[i + 1 - l], rightBB = rightMax[i + 1 - l];
+      lenx = rightBB.x - rightAA.x; leny = rightBB.y - rightAA.y; lenz = rightBB.z - rightAA.z;
+      const float rightS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
+      const float rightCost = rightS * (float)(r - i);
+      const float totalCost = leftCost + rightCost;
+      if (totalCost < cost) { cost = totalCost; split = i; }
+    }
+    if (cost < Cost) { Cost = cost; Axis = axis; Split = split; }
+  }
+  fast_sort(B, l, r, Axis);
+  std::vector<v3>().swap(leftMax); std::vector<v3>().swap(leftMin);
+  std::vector<v3>().swap(rightMax); std::vector<v3>().swap(rightMin);
+  int left, right;
+  if (depth < B.par_depth && cnt > 4096) {
+    // the two subtrees own disjoint ranges of perm: build them concurrently, then splice
+    std::vector<Node> ln, rn;
+    std::thread th([&] { fast_sah(B, ln, l, Split, depth + 1); });
+    fast_sah(B, rn, Split + 1, r, depth + 1);
+    th.join();
+    auto splice = [&](std::vector<Node>& sub) {
+      if (sub.empty()) return 0;
+      const int base = (int)nodes.size();
+      for (Node& x : sub) {
+        if (x.n == 0) { x.left += base; x.right += base; }  // internal: children are local ids >= 1
+        nodes.push_back(x);
+      }
+      return base;
+    };
+    left = splice(ln);
+    right = splice(rn);
+  } else {
+    left = fast_sah(B, nodes, l, Split, depth + 1);
+    right = fast_sah(B, nodes, Split + 1, r, depth + 1);
+  }
+  nd.left = left;
+  nd.right = right;
+  nodes[id] = nd;
+  return id;
+}
+
+void build_sah_fast(std::vector<Tri>& tris, std::vector<Node>& nodes, int n) {
+  const int nt = (int)tris.size();
+  FastBuild B;
+  B.n = n;
+  unsigned hw = std::thread::hardware_concurrency();
+  B.par_depth = 0;
+  while ((1u << B.par_depth) < std::max(1u, hw) * 2u && B.par_depth < 6) B.par_depth++;
+  for (int a = 0; a < 3; a++) B.c[a].resize(nt);
+  B.tmin.resize(nt); B.tmax.resize(nt); B.perm.resize(nt);
+  for (int t = 0; t < nt; t++) {
+    const Tri& x = tris[t];
+    B.c[0][t] = centre(x, 0); B.c[1][t] = centre(x, 1); B.c[2][t] = centre(x, 2);
+    B.tmin[t] = mk(min3(x.p1.x, x.p2.x, x.p3.x), min3(x.p1.y, x.p2.y, x.p3.y), min3(x.p1.z, x.p2.z, x.p3.z));
+    B.tmax[t] = mk(max3(x.p1.x, x.p2.x, x.p3.x), max3(x.p1.y, x.p2.y, x.p3.y), max3(x.p1.z, x.p2.z, x.p3.z));
+    B.perm[t] = t;
+  }
+  std::vector<Node> local;
+  local.reserve(2 * (size_t)nt / std::max(1, n) + 2);
+  fast_sah(B, local, 0, nt - 1, 0);
+  const int base = (int)nodes.size();  // after the dummy node 0
+  for (Node& x : local) {
+    if (x.n == 0) { x.left += base; x.right += base; }
+    nodes.push_back(x);
+  }
+  std::vector<Tri> sorted(nt);
+  for (int i = 0; i < nt; i++) sorted[i] = tris[B.perm[i]];
+  tris.swap(sorted);
+}
+
 void tree_stats(const std::vector<Node>& nodes, int root, int32_t& depth, int32_t& leaves) {
   depth = 0;
   leaves = 0;
@@ -740,7 +877,11 @@ int rts_scene_build_bvh(rts_scene* s, int leaf_size) {
   dummy.AA = mk(1, 1, 0); dummy.BB = mk(0, 1, 0);
   s->nodes.clear();
   s->nodes.push_back(dummy);
-  if (!s->tris.empty()) build_sah(s->tris, s->nodes, 0, (int)s->tris.size() - 1, leaf_size);
+  if (!s->tris.empty()) {
+    const char* lit = getenv("RTS_BVH_LITERAL");  // the line-by-line restatement (checks the fast build)
+    if (lit && atoi(lit)) build_sah(s->tris, s->nodes, 0, (int)s->tris.size() - 1, leaf_size);
+    else build_sah_fast(s->tris, s->nodes, leaf_size);
+  }
   s->built = true;
   return RTS_OK;
 }

@@ -206,3 +206,21 @@ def test_material_update_post_bvh():
     assert np.all(np.all(tri[bunny_post[:10], 6:14] == golden, axis=(1, 2)))
     soa = s.export_soa()
     assert len(soa["materials"]) == 3
+
+
+def test_fast_bvh_build_equals_literal_restatement(monkeypatch):
+    """The parallel index-sort SAH build (default) produces byte-identical triangles and nodes
+    to the line-by-line restatement of buildBVHwithSAH (src/core/BVH.h:110-241)."""
+    import hashlib
+    from rtamd import scene_lib as sl
+
+    def build(literal):
+        monkeypatch.setenv("RTS_BVH_LITERAL", "1" if literal else "0")
+        s = sl.Scene()
+        for o in cf.CONFIGS["C3"].objects:
+            s.add_mesh(cf.load_mesh(o.mesh), cf.MATERIALS[o.material], o.rotate, o.translate, o.scale, o.smooth)
+        s.build_bvh(8)
+        tri, nodes = s.encode()
+        return hashlib.sha256(tri.tobytes()).hexdigest(), hashlib.sha256(nodes.tobytes()).hexdigest()
+
+    assert build(True) == build(False)
