@@ -5,8 +5,8 @@ Workload (default): config C3 = floor + loong_100000 (copper), 1920x1080, maxBou
 HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs.py).
 One *step* = ``--frames-per-step`` (default 512) progressive frames (1 spp each) of the whole
 frame, rendered by one rt_render call per rank over that rank's pixel tiles (frames in flight
-bounded by the 160M-slot path-state budget: 64 at a time on one GPU, all 512 at once on each of
-8 tile-sharded GPUs, so every rank keeps the same work in flight: strong scaling of a fixed
+bounded by the 320Mi-slot path-state budget: 161 at a time on one GPU, all 512 at once on each
+of 8 tile-sharded GPUs, so every rank keeps plenty of work in flight: strong scaling of a fixed
 frame budget without a per-rank latency floor penalty), followed by the
 frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
 torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.

@@ -50,7 +50,8 @@ enum {
 };
 
 /* Frames per kernel batch; the path-state budget (216 B per pixel-frame, RT_MAX_SLOTS, default
- * 160M) bounds it too: 64 frames at 1920x1080 on one GPU, 512 on each of 8 tile-sharded GPUs. */
+ * 320Mi slots = 69 GB) bounds it too: 161 frames at 1920x1080 on one GPU, all 512 of a bench
+ * step on each of 8 tile-sharded GPUs. */
 enum { RT_MAX_FRAMES_PER_LAUNCH = 1024 };
 
 /* Disney material (src/core/Material.h:25-46), 24 floats, same layout as rts_material. */

@@ -387,8 +387,8 @@ int rt_create(int hip_device, rt_ctx** out) {
   c->own_stream = true;
   if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
   if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
-  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 32 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -676,7 +676,7 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   // 64 frames at 1080p); the state grows on demand in rt_render_async, so interactive 1-frame
   // use stays small.  More frames per launch amortise the per-pass latency floor of the few
   // longest rays (C3: 16 frames 1.07, 32 frames 0.99, 64 frames 0.94 ms/frame).
-  size_t max_slots = size_t(160) << 20;
+  size_t max_slots = size_t(320) << 20;  // 216 B each: 69 GB of the 288 GB HBM3E (C3: 160 frames in flight; 160 M slots: -1.8%)
   if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
   c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / nv));
   int rc = alloc_wavefront(c, nv);
@@ -978,6 +978,12 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->trace_ms = c->trace_ms;
   st->trace_iters = h[5];
   st->trace_iters_max = h[6];
+#ifdef RT_SHADE_PROF  // development variant: wave cycles per wf_shade phase (stats 16..21)
+  unsigned long long ph[6];
+  HIPCHK(c, hipMemcpy(ph, c->d_stats + 16, sizeof(ph), hipMemcpyDeviceToHost));
+  fprintf(stderr, "[shade-prof] sort %llu consume %llu nee %llu sample %llu store %llu flush %llu\n",
+          ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+#endif
   return RT_OK;
 }
 
@@ -985,7 +991,7 @@ int rt_stats_reset(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
+  HIPCHK(c, hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)));
   c->kernel_ms = 0.0;
   c->launches = 0;
   c->trace_ms = 0.0;

@@ -390,6 +390,9 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 1
 #endif
+#ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s
+#define RT_REFILL_MIN 16
+#endif
 template <bool COUNT, int MODE, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE))) void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -450,7 +453,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WP
     // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
     // queue so the last rays still spread over all waves.
     const unsigned long long idle = __ballot(!busy);
-    if (idle && !drained) {
+    // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
+    // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
+    // than the lanes it brings back
+    if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
       if (pool_next >= pool_end) {
         const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : 64u;
         unsigned int base = 0;
@@ -663,6 +669,13 @@ RTD int shade_key(const KParams& P, const WFState& S, int path) {
 #define RT_SHADE_WPE 4
 #endif
 constexpr int SH_SUB = RT_SH_SUB;
+#ifdef RT_SHADE_PROF  // development variant: wave cycles per phase -> stats[16..21]
+#define SHP_DECL unsigned long long shp[6] = {0, 0, 0, 0, 0, 0}, shp_t = clock64();
+#define SHP_MARK(i) { const unsigned long long _n = clock64(); shp[i] += _n - shp_t; shp_t = _n; }
+#else
+#define SHP_DECL
+#define SHP_MARK(i)
+#endif
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
   __shared__ int lq[2 * 256 * SH_SUB];
@@ -679,6 +692,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
+  SHP_DECL
   for (unsigned int base = blockIdx.x * (256u * SH_SUB); base < na; base += gridDim.x * (256u * SH_SUB)) {
   // ---- group the block's paths by what they will execute (block-local counting sort in LDS):
   // divergence between a continuation that missed (env lookup) and one that hit (a full BSDF
@@ -720,6 +734,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     if ((unsigned)sub * 256u + threadIdx.x < nblk) lsort[lofs[skey[sub]] + srank[sub]] = spath[sub];
   }
   __syncthreads();
+  SHP_MARK(0)
   for (int sub = 0; sub < SH_SUB; sub++) {
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
@@ -836,6 +851,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       }
     }
 
+    SHP_MARK(1)
+#ifdef RT_SHADE_PROF
+    unsigned long long shp_mid = 0;
+#endif
     // ------------------------------------------------------------- next bounce
     f3 cnee = splat(0.0f), cmed = splat(0.0f);
     uint32_t nflags = 0;
@@ -915,6 +934,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         qShadow = true;
         nflags |= PF_SHADOW;
       }
+#ifdef RT_SHADE_PROF
+      shp_mid = clock64();
+#endif
       // BSDF sample (RT:1408-1474)
       int g = P.loop_num[frame] + 1;
       g = g ^ (g >> 1);
@@ -972,6 +994,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       }
     }
 
+#ifdef RT_SHADE_PROF
+    for (int off = 32; off > 0; off >>= 1) shp_mid = max(shp_mid, (unsigned long long)__shfl_xor((long long)shp_mid, off));
+    if (shp_mid > shp_t) { shp[2] += shp_mid - shp_t; shp_t = shp_mid; }
+    SHP_MARK(3)
+#endif
     // ----------------------------------------------------------- progressive blend
     if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
       S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
@@ -1002,6 +1029,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     if (qCont) lq[qs + (qShadow ? 1u : 0u)] = path << 1;
     const unsigned int ai = wave_lds_append(&lc[1], keep ? 1u : 0u);
     if (keep) la[ai] = path;
+    SHP_MARK(4)
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1012,7 +1040,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue[out][lc[2] + j] = lq[j];
   for (unsigned int j = threadIdx.x; j < lc[1]; j += 256u) S.active[out][lc[3] + j] = la[j];
   __syncthreads();
+  SHP_MARK(5)
   }
+#ifdef RT_SHADE_PROF
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < 6; i++) atomicAdd(&P.stats[16 + i], shp[i]);
+#endif
   // per-wave counter flush
   for (int off = 32; off > 0; off >>= 1) {
     nrays += __shfl_xor(nrays, off);
