@@ -135,9 +135,8 @@ void pack_material(const rt_material& m, float* o) {
 // * Leaf rank = position of the leaf in the reference's left-first DFS; gn[k].ref.z = rank of
 //   the first leaf of node k's right subtree; trin[3t+1].w = rank of triangle t's leaf.  These
 //   let the 4-wide traversal break exact distance ties the way the reference's visit order does.
-// * A QNode replaces a binary node and up to two levels below it: its slots start as the two
-//   children and the internal slot with the largest surface area is split until there are 4.
-//   Boxes are copied bit for bit.  A (grand)child box can only be hit when every box above it is
+// * A QNode replaces a binary node and a cut of its subtree with at most 4 slots, chosen by the
+//   SAH-optimal collapse below (or greedily, largest area first).  Boxes are copied bit for bit.  A (grand)child box can only be hit when every box above it is
 //   (children are min/max over subsets, and the slab arithmetic is monotone), so the 4-wide
 //   traversal reaches exactly the reference's leaves.
 // Returns false (binary traversal only) when a triangle belongs to two leaves.
@@ -184,23 +183,81 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     for (int k = 0; k < 3; k++) e[k] = (double)s.hi[k] - (double)s.lo[k];
     return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
   };
+  // Which binary nodes become 4-wide nodes.  Default: the collapse that minimises the summed
+  // surface area of the 4-wide nodes (the SAH traversal cost; the leaves and their cost are
+  // fixed): f(n, k) = least area of 4-wide roots covering n's subtree with at most k slots,
+  // f(n, 1) = A(n) + min_j f(L, j) + f(R, 4 - j), f(n, k) = min(f(n, 1), min_j f(L, j) + f(R, k - j)).
+  // RT_COLLAPSE=greedy: open the largest-area internal slot until there are four.
+  const char* ce = getenv("RT_COLLAPSE");
+  const bool greedy = ce && strcmp(ce, "greedy") == 0;
+  const size_t nb = gn.size();
+  std::vector<double> f(nb * 5, 0.0);
+  std::vector<signed char> split(nb * 5, 0);  // 0: keep the node as one slot, j > 0: j slots to the left
+  auto fr = [&](int r, int k) -> double { return is_leaf(r) ? 0.0 : f[(size_t)r * 5 + k]; };
+  if (!greedy && !is_leaf(root)) {
+    std::function<void(int)> dp = [&](int b) {
+      Slot L, R;
+      kids(b, L, R);
+      if (!is_leaf(L.ref)) dp(L.ref);
+      if (!is_leaf(R.ref)) dp(R.ref);
+      Slot U = L;
+      for (int k = 0; k < 3; k++) { U.lo[k] = std::min(L.lo[k], R.lo[k]); U.hi[k] = std::max(L.hi[k], R.hi[k]); }
+      double open = 1e300;
+      int jo = 1;
+      for (int j = 1; j <= 3; j++) {
+        const double c = fr(L.ref, j) + fr(R.ref, 4 - j);
+        if (c < open) { open = c; jo = j; }
+      }
+      f[(size_t)b * 5 + 1] = area(U) + open;
+      split[(size_t)b * 5 + 1] = (signed char)jo;  // the split of the node's own 4-wide record
+      for (int k = 2; k <= 4; k++) {
+        double best = f[(size_t)b * 5 + 1];
+        int bj = 0;
+        for (int j = 1; j < k; j++) {
+          const double c = fr(L.ref, j) + fr(R.ref, k - j);
+          if (c < best) { best = c; bj = j; }
+        }
+        f[(size_t)b * 5 + k] = best;
+        split[(size_t)b * 5 + k] = (signed char)bj;
+      }
+    };
+    dp(root);
+  }
+  // DP reconstruction: the slots that binary subtree s contributes when given k of them
+  std::function<void(const Slot&, int, std::vector<Slot>&)> collect = [&](const Slot& s, int k, std::vector<Slot>& out) {
+    if (is_leaf(s.ref) || k == 1 || split[(size_t)s.ref * 5 + k] == 0) { out.push_back(s); return; }
+    const int j = split[(size_t)s.ref * 5 + k];
+    Slot L, R;
+    kids(s.ref, L, R);
+    collect(L, j, out);
+    collect(R, k - j, out);
+  };
   qdepth = 1;
   std::function<int(int, int)> build = [&](int b, int depth) -> int {
     qdepth = std::max(qdepth, depth);
     const int idx = (int)qn.size();
     qn.push_back(rtd::QNode{});
-    std::vector<Slot> sl(2);
-    kids(b, sl[0], sl[1]);
-    while (sl.size() < 4) {
-      int pick = -1;
-      double pa = -1.0;
-      for (size_t i = 0; i < sl.size(); i++)
-        if (!is_leaf(sl[i].ref) && area(sl[i]) > pa) { pa = area(sl[i]); pick = (int)i; }
-      if (pick < 0) break;
-      Slot x, y;
-      kids(sl[pick].ref, x, y);
-      sl[pick] = x;
-      sl.insert(sl.begin() + pick + 1, y);
+    std::vector<Slot> sl;
+    if (greedy) {
+      sl.resize(2);
+      kids(b, sl[0], sl[1]);
+      while (sl.size() < 4) {
+        int pick = -1;
+        double pa = -1.0;
+        for (size_t i = 0; i < sl.size(); i++)
+          if (!is_leaf(sl[i].ref) && area(sl[i]) > pa) { pa = area(sl[i]); pick = (int)i; }
+        if (pick < 0) break;
+        Slot x, y;
+        kids(sl[pick].ref, x, y);
+        sl[pick] = x;
+        sl.insert(sl.begin() + pick + 1, y);
+      }
+    } else {
+      Slot L, R;
+      kids(b, L, R);
+      const int j = split[(size_t)b * 5 + 1];
+      collect(L, j, sl);
+      collect(R, 4 - j, sl);
     }
     int refs[4] = {rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY};
     for (size_t i = 0; i < sl.size(); i++) refs[i] = is_leaf(sl[i].ref) ? sl[i].ref : build(sl[i].ref, depth + 1);
