@@ -298,7 +298,7 @@ int occupancy(rt_ctx* c) {
   c->blocks_per_cu = std::max(1, bpc);
   c->block_lds = lds;
   // wavefront traversal: short LDS stack + global overflow
-  int kl = 12;
+  int kl = 8;  // 16 KiB per block: LDS leaves room for 8 waves/SIMD (12 entries: 6; C3 5853 -> 5959 at 10, 6155 at 8 with the dual schedule at 8 waves)
   if (const char* e = getenv("RT_LDS_STACK")) kl = atoi(e);
   kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;

@@ -393,8 +393,12 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s
 #define RT_REFILL_MIN 16
 #endif
+#ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
+#define RT_TRACE_WPE_DUAL 8
+#endif
 template <bool COUNT, int MODE, bool WIDE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE))) void wf_trace(const WFParams W) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == TM_DUAL ? RT_TRACE_WPE_DUAL : RT_TRACE_WPE)))
+void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
@@ -650,6 +654,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WP
 #ifndef RT_SH_SUB
 #define RT_SH_SUB 4
 #endif
+#ifndef RT_SH_EARLY  // issue all path-state loads before the flags arrive
+#define RT_SH_EARLY 1
+#endif
+#ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0)
+#define RT_SH_KEY_MAT 1
+#endif
 constexpr int SH_KEYS = 8;  // 0: no continuation hit; 1 + material id % 7: continuation hit
 #ifndef RT_SH_SORT_MIN
 #define RT_SH_SORT_MIN (1u << 24)
@@ -660,10 +670,13 @@ constexpr unsigned int SH_SORT_MIN = RT_SH_SORT_MIN;  // active paths from which
 // the hit material
 RTD int shade_key(const KParams& P, const WFState& S, int path) {
   const uint32_t flags = S.s5[path].z;
-  if (!(flags & PF_CONT)) return 0;
   const int t = S.res[2 * path].x;
-  if (t < 0) return 0;
+  if (!(flags & PF_CONT) || t < 0) return 0;
+#if RT_SH_KEY_MAT
   return 1 + __float_as_int(P.trin[3 * t].w) % (SH_KEYS - 1);
+#else
+  return 1;
+#endif
 }
 #ifndef RT_SHADE_WPE  // 4 waves/SIMD (<= 128 VGPRs, 12 B/lane spill): shade -8% vs the natural 3
 #define RT_SHADE_WPE 4
@@ -752,17 +765,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     int mat = 0;
     if (live) {
       a5 = S.s5[path];
+#if RT_SH_EARLY
+      // every load of the path's state issues at once: camera paths exist only in pass 0 (a
+      // uniform test), so no load waits for the flags; the flags still decide what is used
+      int2 rsh = make_int2(0, 0);
+      if (W.pass != 0) {
+        a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path]; a3 = S.s3[path];
+        rsh = S.res[2 * path + 1];
+      }
+      const int2 rc0 = S.res[2 * path];
+      const float4 oo0 = S.ro[path], dd0 = S.rd[path];
+#endif
       wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
       if (!(flags & PF_CAMERA)) {
+#if !RT_SH_EARLY
         a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path];
+#endif
         hist = xyz(a0); evp = a0.w;
         Lo = xyz(a1);
         evf = xyz(a2);
         Le0 = mk3(a1.w, a2.w, 0.0f);
+#if !RT_SH_EARLY
         a3 = S.s3[path];
+        const int2 rsh = S.res[2 * path + 1];
+#endif
         Le0.z = a3.w;
         // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
-        if ((flags & PF_SHADOW) && S.res[2 * path + 1].x < 0) Lo = Lo + xyz(a3);
+        if ((flags & PF_SHADOW) && rsh.x < 0) Lo = Lo + xyz(a3);
         // ---- pending medium-emissive term (RT:1437-1439)
         if (flags & PF_CMED) {
           a4 = S.s4[path];
@@ -773,8 +802,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         fin = Le0 + Lo;
         doFinish = true;
       } else {
+#if RT_SH_EARLY
+        const int2 r = rc0;
+        const float4 oo = oo0, dd = dd0;
+#else
         const int2 r = S.res[2 * path];
         const float4 oo = S.ro[path], dd = S.rd[path];
+#endif
         const f3 ro = xyz(oo), rd = xyz(dd);
         if (r.x >= 0) {
           const int tri = r.x;
