@@ -654,8 +654,8 @@ void wf_trace(const WFParams W) {
 #ifndef RT_SH_SUB
 #define RT_SH_SUB 4
 #endif
-#ifndef RT_SH_EARLY  // issue all path-state loads before the flags arrive
-#define RT_SH_EARLY 1
+#ifndef RT_SH_EARLY  // 1: issue every path-state load before the flags arrive (measured -1.4%)
+#define RT_SH_EARLY 0
 #endif
 #ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0)
 #define RT_SH_KEY_MAT 1

@@ -115,6 +115,7 @@ class FrameParams:
 
 
 _lib = None
+_variants: dict = {}
 
 
 def _share_torch_hip_runtime() -> None:
@@ -128,41 +129,51 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
-def lib() -> C.CDLL:
+def lib(path: Optional[str] = None) -> C.CDLL:
+    """librtamd.so (or RTAMD_LIB, or an explicit build variant: each path is loaded once, with
+    RTLD_LOCAL, so development variants can coexist in one process for A/B timing)."""
     global _lib
+    _share_torch_hip_runtime()  # before the first librtamd load (see above)
+    if path is not None:
+        path = str(path)
+        if path not in _variants:
+            _variants[path] = _bind(C.CDLL(path))
+        return _variants[path]
     if _lib is None:
-        _share_torch_hip_runtime()
-        L = C.CDLL(os.environ.get("RTAMD_LIB") or str(lib_path("librtamd.so")))
-        vp = C.c_void_p
-        L.rt_create.argtypes = [C.c_int, C.POINTER(vp)]
-        L.rt_destroy.argtypes = [vp]
-        L.rt_last_error.argtypes = [vp]
-        L.rt_last_error.restype = C.c_char_p
-        L.rt_device_info.argtypes = [vp, _i32p, _i32p, _i32p]
-        L.rt_set_scene.argtypes = [vp, C.POINTER(RtSceneSoa)]
-        L.rt_set_scene_encoded.argtypes = [vp, _f32p, C.c_int32, _f32p, C.c_int32]
-        L.rt_update_materials.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(RtMaterial)]
-        L.rt_set_env.argtypes = [vp, _f32p, _f32p, C.c_int32, C.c_int32, C.c_int32]
-        L.rt_resize.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(RtTiling)]
-        L.rt_reset.argtypes = [vp]
-        L.rt_set_loop_num.argtypes = [vp, C.c_int32]
-        L.rt_get_loop_num.argtypes = [vp, _i32p]
-        L.rt_clear_accum.argtypes = [vp]
-        L.rt_render_async.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32]
-        L.rt_render.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(RtStats)]
-        L.rt_synchronize.argtypes = [vp]
-        L.rt_stats_get.argtypes = [vp, C.POINTER(RtStats)]
-        L.rt_stats_reset.argtypes = [vp]
-        L.rt_get_stream.argtypes = [vp, C.POINTER(vp)]
-        L.rt_set_stream.argtypes = [vp, vp]
-        L.rt_read_accum.argtypes = [vp, _f32p, C.c_int32]
-        L.rt_write_accum.argtypes = [vp, _f32p, C.c_int32]
-        L.rt_accum_device.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), _i32p, _i32p]
-        L.rt_copy_accum_device.argtypes = [vp, vp, C.c_size_t]
-        L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
-        L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
-        _lib = L
+        _lib = _bind(C.CDLL(os.environ.get("RTAMD_LIB") or str(lib_path("librtamd.so"))))
     return _lib
+
+
+def _bind(L: C.CDLL) -> C.CDLL:
+    vp = C.c_void_p
+    L.rt_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.rt_destroy.argtypes = [vp]
+    L.rt_last_error.argtypes = [vp]
+    L.rt_last_error.restype = C.c_char_p
+    L.rt_device_info.argtypes = [vp, _i32p, _i32p, _i32p]
+    L.rt_set_scene.argtypes = [vp, C.POINTER(RtSceneSoa)]
+    L.rt_set_scene_encoded.argtypes = [vp, _f32p, C.c_int32, _f32p, C.c_int32]
+    L.rt_update_materials.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(RtMaterial)]
+    L.rt_set_env.argtypes = [vp, _f32p, _f32p, C.c_int32, C.c_int32, C.c_int32]
+    L.rt_resize.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(RtTiling)]
+    L.rt_reset.argtypes = [vp]
+    L.rt_set_loop_num.argtypes = [vp, C.c_int32]
+    L.rt_get_loop_num.argtypes = [vp, _i32p]
+    L.rt_clear_accum.argtypes = [vp]
+    L.rt_render_async.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32]
+    L.rt_render.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(RtStats)]
+    L.rt_synchronize.argtypes = [vp]
+    L.rt_stats_get.argtypes = [vp, C.POINTER(RtStats)]
+    L.rt_stats_reset.argtypes = [vp]
+    L.rt_get_stream.argtypes = [vp, C.POINTER(vp)]
+    L.rt_set_stream.argtypes = [vp, vp]
+    L.rt_read_accum.argtypes = [vp, _f32p, C.c_int32]
+    L.rt_write_accum.argtypes = [vp, _f32p, C.c_int32]
+    L.rt_accum_device.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), _i32p, _i32p]
+    L.rt_copy_accum_device.argtypes = [vp, vp, C.c_size_t]
+    L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
+    L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
+    return L
 
 
 def _fp(a):
@@ -176,8 +187,8 @@ def _ip(a):
 class Renderer:
     """One HIP device's path tracer (one per rank in multi-GPU runs)."""
 
-    def __init__(self, device: int = 0):
-        self._L = lib()
+    def __init__(self, device: int = 0, lib_path: Optional[str] = None):
+        self._L = lib(lib_path)
         h = C.c_void_p()
         rc = self._L.rt_create(int(device), C.byref(h))
         if rc != RT_OK:
