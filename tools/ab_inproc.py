@@ -54,7 +54,7 @@ for name, path, env in specs:
         r.set_scene_soa(sd.soa, sd.nodes)
         r.set_env(*env_maps)
         r.resize(W, H)
-        r.render(fp, ro[:min(len(ro), 64)])  # allocations, code objects
+        r.render(fp, ro)  # full-size allocations once (a smaller first call re-allocates later), code objects
         r.synchronize()
     finally:
         for k, v in saved.items():
