@@ -654,11 +654,11 @@ void wf_trace(const WFParams W) {
 #ifndef RT_SH_SUB
 #define RT_SH_SUB 4
 #endif
-#ifndef RT_SH_EARLY  // 1: issue every path-state load before the flags arrive (measured -1.4%)
-#define RT_SH_EARLY 0
+#ifndef RT_SH_EARLY  // issue every path-state load before the flags arrive (+0.6%, tools/ab_proc.py)
+#define RT_SH_EARLY 1
 #endif
-#ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0)
-#define RT_SH_KEY_MAT 1
+#ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0: +1.0%)
+#define RT_SH_KEY_MAT 0
 #endif
 constexpr int SH_KEYS = 8;  // 0: no continuation hit; 1 + material id % 7: continuation hit
 #ifndef RT_SH_SORT_MIN
