@@ -84,6 +84,7 @@ struct rt_ctx {
   // bounces overlaps the other's busy passes; blends stay in frame order (events).
   static constexpr int MAX_GROUPS = 4;
   int n_groups = 2;
+  int stages = 1;                  // frames of a group start over this many passes (RT_STAGES)
   rtd::WFState wfg[MAX_GROUPS]{};
   hipStream_t aux[MAX_GROUPS] = {};
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
@@ -443,6 +444,7 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
   c->own_stream = true;
   if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
+  if (const char* e = getenv("RT_STAGES")) c->stages = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 32 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)) != hipSuccess) {
@@ -908,14 +910,20 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           HIPCHK(c, hipStreamWaitEvent(sg[g], prev_stagger, 0));
           c->event_pool.push_back(prev_stagger);  // reusable once the wait is enqueued
         }
-        const unsigned int gen_grid = std::max(1u, std::min<unsigned int>(4096u, (slots_g[g] + 255) / 256));
         HIPCHK(c, hipMemsetAsync(WP.S.cnt, 0, 64, sg[g]));
-        WP.pass = 0;
-        hipLaunchKernelGGL(rtd::wf_gen, dim3(gen_grid), dim3(256), 0, sg[g], WP);
-        HIPCHK(c, hipGetLastError());
         prev_stagger = nullptr;
-        for (int pass = 0; pass <= last_pass; pass++) {
+        // the group's frames start in `stages` steps, one per pass (see wf_gen)
+        const int nfg = WP.n_frames;
+        const int stages = std::max(1, std::min(c->stages, nfg));
+        for (int pass = 0; pass <= last_pass + stages - 1; pass++) {
           WP.pass = pass;
+          if (pass < stages) {
+            WP.gen_f0 = pass * nfg / stages;
+            WP.gen_f1 = (pass + 1) * nfg / stages;
+            const unsigned int runs = ((unsigned)(WP.gen_f1 - WP.gen_f0) * (unsigned)c->n_valid + rtd::GEN_RUN - 1) / rtd::GEN_RUN;
+            hipLaunchKernelGGL(rtd::wf_gen, dim3(std::max(1u, std::min(runs, 8192u))), dim3(256), 0, sg[g], WP);
+            HIPCHK(c, hipGetLastError());
+          }
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));

@@ -61,6 +61,7 @@ struct WFParams {
   WFState S;
   int n_frames;  // frames in flight: slots = n_frames * K.n_work
   int pass;      // bounce pass: queue/active set pass&1 in, (pass+1)&1 out
+  int gen_f0, gen_f1;  // wf_gen: the frames [gen_f0, gen_f1) whose camera paths start this pass
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -108,31 +109,45 @@ RTD unsigned int wave_lds_append(unsigned int* lcount, unsigned int n) {
 }
 
 // ------------------------------------------------------------------------------- gen
+// Camera paths of frames [gen_f0, gen_f1) (RT:1520-1527), appended to the ray queue and active
+// list of this pass.  Frames start in stages (one stage per pass for the first passes): every
+// pass then mixes fresh camera paths with deeper bounces of earlier stages instead of the batch
+// ending in a long tail of nearly empty passes.  A block writes a contiguous run of GEN_RUN
+// slots behind one claim per list.
+constexpr unsigned int GEN_RUN = 256u * 8u;
 __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
+  const int in = W.pass & 1;
   const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
   const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
   const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
-  const unsigned int total = (unsigned)W.n_frames * P.n_work;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S.cnt[0] = total;  // queue 0 and active list 0 are the identity over all slots
-    S.cnt[2] = total;
-  }
-  for (unsigned int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
-    const unsigned int f = slot / P.n_work;
-    const unsigned int w = slot - f * P.n_work;
-    const unsigned int xy = S.pix_xy[w];
-    const int px = (int)(xy & 0xffffu), py = (int)(xy >> 16);
-    const float u = ((float)px + 0.5f) / (float)P.W;  // TexCoords (vertex_shader.glsl)
-    const float v = ((float)py + 0.5f) / (float)P.H;
-    const uint32_t wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * (u * v));  // R5
-    const f3 d = normalize(lbc + (u * 2.0f * P.half_w) * right + (v * 2.0f * P.half_h) * up);  // R6
-    S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
-    S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
-    S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
-    S.queue[0][slot] = (int)(slot << 1);
-    S.active[0][slot] = (int)slot;
+  const unsigned int s0 = (unsigned)W.gen_f0 * P.n_work, s1 = (unsigned)W.gen_f1 * P.n_work;
+  __shared__ unsigned int qbase, abase;
+  for (unsigned int run = s0 + blockIdx.x * GEN_RUN; run < s1; run += gridDim.x * GEN_RUN) {
+    const unsigned int n = min(GEN_RUN, s1 - run);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      qbase = atomicAdd(&S.cnt[in], n);
+      abase = atomicAdd(&S.cnt[2 + in], n);
+    }
+    __syncthreads();
+    for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
+      const unsigned int slot = run + j;
+      const unsigned int f = slot / P.n_work;
+      const unsigned int w = slot - f * P.n_work;
+      const unsigned int xy = S.pix_xy[w];
+      const int px = (int)(xy & 0xffffu), py = (int)(xy >> 16);
+      const float u = ((float)px + 0.5f) / (float)P.W;  // TexCoords (vertex_shader.glsl)
+      const float v = ((float)py + 0.5f) / (float)P.H;
+      const uint32_t wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * (u * v));  // R5
+      const f3 d = normalize(lbc + (u * 2.0f * P.half_w) * right + (v * 2.0f * P.half_h) * up);  // R6
+      S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
+      S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+      S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
+      S.queue[in][qbase + j] = (int)(slot << 1);
+      S.active[in][abase + j] = (int)slot;
+    }
   }
 }
 
