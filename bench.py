@@ -5,8 +5,8 @@ Workload (default): config C3 = floor + loong_100000 (copper), 1920x1080, maxBou
 HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs.py).
 One *step* = ``--frames-per-step`` (default 512) progressive frames (1 spp each) of the whole
 frame, rendered by one rt_render call per rank over that rank's pixel tiles (frames in flight
-bounded by the 320Mi-slot path-state budget: 161 at a time on one GPU, all 512 at once on each
-of 8 tile-sharded GPUs, so every rank keeps plenty of work in flight: strong scaling of a fixed
+all in flight at once (rt_set_max_paths: 216 B per pixel-frame, 229 GB of HBM3E on one GPU,
+29 GB per rank on 8 tile-sharded GPUs), so every rank keeps plenty of work in flight: strong scaling of a fixed
 frame budget without a per-rank latency floor penalty), followed by the
 frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
 torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
@@ -129,6 +129,11 @@ def main() -> int:
     r.resize(W, H, tile=args.tile, rank=rank, world=world)
     info = r.device_info()
     ad = r.accum_device()
+    # path-state budget: a whole step's frames in flight at once (216 B per pixel-frame: 229 GB
+    # of HBM3E for 512 frames of 1080p on one GPU, 29 GB per rank at N = 8); the library runs
+    # fewer at a time if they do not fit
+    path_slots = F * ad["local_tiles"] * args.tile * args.tile
+    r.set_max_paths(path_slots)
     nfloat = ad["bytes"] // 4
     local = torch.empty(nfloat, dtype=torch.float32, device="cuda")
     gathered = torch.empty(world * nfloat, dtype=torch.float32, device="cuda") if rank == 0 else None
@@ -207,7 +212,7 @@ def main() -> int:
                 "randOrigin from glibc srand(20221002)",
         "config": {"workload": f"{cfg.name}: {cfg.note}; {W}x{H}, maxBounce 8, BSDF+MIS+env",
                    "width": W, "height": H, "frames_per_step": F, "spp_timed": steps * F,
-                   "tile": args.tile, "parallelism": f"pixel-tiles x{world} + frame-end gather",
+                   "tile": args.tile, "path_slots_per_rank": path_slots, "parallelism": f"pixel-tiles x{world} + frame-end gather",
                    "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
         "kernel": {"name": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "launches": st["trace_launches"],
                    "render_call_ms": round(launch_ms, 4), "render_calls": st["launches"],
@@ -228,7 +233,7 @@ def main() -> int:
     if pmc.exists():
         p = json.loads(pmc.read_text())
         if (p.get("kernel") == "wf_trace" and p.get("width") == W and p.get("height") == H
-                and p.get("frames_per_launch") == F):
+                and p.get("frames_per_launch") == F and p.get("path_slots_per_rank") == path_slots):
             traffic = p.get("hbm_bytes_per_launch")
     if cnt is not None:
         # dominant kernel = wf_trace: the reference traversal's bytes per ray (SURVEY §8(d) terms of

@@ -132,6 +132,11 @@ int rt_set_loop_num(rt_ctx* ctx, int32_t loop_num);
 int rt_get_loop_num(const rt_ctx* ctx, int32_t* loop_num);
 /* Clear this rank's accumulation to zero (fresh FBO contents). */
 int rt_clear_accum(rt_ctx* ctx);
+/* Path-state budget in pixel-frames (216 B each): frames in flight per launch = slots / pixels of
+ * this rank, at most RT_MAX_FRAMES_PER_LAUNCH.  0 = RT_MAX_SLOTS from the environment or the
+ * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL
+ * counterpart: the fragment shader has one path per pixel in flight. */
+int rt_set_max_paths(rt_ctx* ctx, uint64_t slots);
 
 /* Enqueue n_frames progressive frames (one randOrigin per frame) on the ctx stream.  Each
  * frame first applies main.cpp:175 (LoopNum++ unless it reached max_iterations). */

@@ -90,6 +90,7 @@ struct rt_ctx {
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
+  size_t max_slots_req = 0;        // rt_set_max_paths (0: RT_MAX_SLOTS or the 320 Mi default)
 };
 
 namespace {
@@ -394,8 +395,20 @@ hipEvent_t take_event(rt_ctx* c) {
   return e;
 }
 
+// Frames in flight per launch = path-state budget / pixels of this rank.  The state grows on
+// demand in rt_render_async, so interactive 1-frame use stays small.  More frames per launch
+// amortise the per-pass latency floor of the few longest rays (C3 1080p: 16 frames 1.07, 64
+// frames 0.94 ms/frame; 161 vs 80 frames +1.8%, all 512 of a bench step at once +2.2%).
+void update_frames_cap(rt_ctx* c, size_t nv) {
+  size_t max_slots = size_t(320) << 20;  // 216 B each: 69 GB of the 288 GB HBM3E
+  if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
+  if (c->max_slots_req) max_slots = c->max_slots_req;
+  c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / std::max<size_t>(1, nv)));
+}
+
 // Path-state buffers of the wavefront path: `paths` slots for each of the n_groups frame
-// groups, carved from one allocation (216 B per slot + counters).
+// groups, carved from one allocation (216 B per slot + counters).  RT_ERR_NOMEM when HBM
+// cannot hold them (the caller then runs fewer frames at a time).
 int alloc_wavefront(rt_ctx* c, size_t paths) {
   if (c->wf_mem && c->wf_paths >= paths) return RT_OK;
   if (c->wf_mem) {  // grow: earlier launches on the streams may still read the old state
@@ -405,7 +418,14 @@ int alloc_wavefront(rt_ctx* c, size_t paths) {
   }
   const size_t P = std::max<size_t>(paths, 64);
   const size_t per = P * (6 * 16 + 4 * 16 + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
-  HIPCHK(c, hipMalloc(&c->wf_mem, per * c->n_groups));
+  const hipError_t me = hipMalloc(&c->wf_mem, per * c->n_groups);
+  if (me == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    c->wf_mem = nullptr;
+    c->wf_paths = 0;
+    return fail(c, RT_ERR_NOMEM, "path state does not fit in device memory");
+  }
+  HIPCHK(c, me);
   char* p = static_cast<char*>(c->wf_mem);
   auto carve = [&](size_t n) { char* q = p; p += (n + 255) & ~size_t(255); return q; };
   for (int g = 0; g < c->n_groups; g++) {
@@ -731,13 +751,7 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
   }
-  // frames in flight: path-state budget of 160M slots (216 B each, ~35 GB of the 288 GB HBM:
-  // 64 frames at 1080p); the state grows on demand in rt_render_async, so interactive 1-frame
-  // use stays small.  More frames per launch amortise the per-pass latency floor of the few
-  // longest rays (C3: 16 frames 1.07, 32 frames 0.99, 64 frames 0.94 ms/frame).
-  size_t max_slots = size_t(320) << 20;  // 216 B each: 69 GB of the 288 GB HBM3E (C3: 160 frames in flight; 160 M slots: -1.8%)
-  if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
-  c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / nv));
+  update_frames_cap(c, nv);
   int rc = alloc_wavefront(c, nv);
   if (rc) return rc;
   c->wf.pix_xy = c->d_pix;
@@ -757,6 +771,13 @@ int rt_set_loop_num(rt_ctx* c, int32_t n) {
   c->loop_num = n;
   return RT_OK;
 }
+int rt_set_max_paths(rt_ctx* c, uint64_t slots) {
+  if (!c) return RT_ERR_ARG;
+  c->max_slots_req = (size_t)slots;
+  if (c->frame_set) update_frames_cap(c, (size_t)c->n_valid);
+  return RT_OK;
+}
+
 int rt_get_loop_num(const rt_ctx* c, int32_t* n) {
   if (!c || !n) return RT_ERR_ARG;
   *n = c->loop_num;
@@ -779,8 +800,13 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   HIPCHK(c, hipSetDevice(c->device));
   if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
     const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
-    const int per_group = (std::min(c->frames_cap, (int)n_frames) + c->n_groups - 1) / c->n_groups;
-    const int rc = alloc_wavefront(c, (size_t)per_group * nv);
+    int rc;
+    while (true) {  // a budget larger than free HBM runs fewer frames at a time
+      const int per_group = (std::min(c->frames_cap, (int)n_frames) + c->n_groups - 1) / c->n_groups;
+      rc = alloc_wavefront(c, (size_t)per_group * nv);
+      if (rc != RT_ERR_NOMEM || per_group <= 1) break;
+      c->frames_cap = std::max(1, std::min(c->frames_cap, (int)n_frames) / 2);
+    }
     if (rc) return rc;
     for (int g = 1; g < c->n_groups; g++)
       if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));

@@ -33,7 +33,7 @@ ABI_SYMBOLS = (
     "rt_update_materials", "rt_set_env", "rt_resize", "rt_reset", "rt_set_loop_num", "rt_get_loop_num",
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
-    "rt_assemble_frame", "rt_tonemap",
+    "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -173,6 +173,7 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_copy_accum_device.argtypes = [vp, vp, C.c_size_t]
     L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
     L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
+    L.rt_set_max_paths.argtypes = [vp, C.c_uint64]
     return L
 
 
@@ -282,6 +283,10 @@ class Renderer:
         v = C.c_int32()
         self._check(self._L.rt_get_loop_num(self._h, C.byref(v)), "rt_get_loop_num")
         return v.value
+
+    def set_max_paths(self, slots: int) -> None:
+        """Path-state budget in pixel-frames (0: the library default); see rt_abi.h."""
+        self._check(self._L.rt_set_max_paths(self._h, int(slots)), "rt_set_max_paths")
 
     def clear_accum(self) -> None:
         self._check(self._L.rt_clear_accum(self._h), "rt_clear_accum")
