@@ -149,3 +149,26 @@ def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
             r.close()
     assert bit_mismatch(img, ref)[0] == 0.0
     assert bit_mismatch(host[..., :3], ref)[0] == 0.0
+
+
+def test_path_budget_beyond_device_memory_falls_back(env_maps):
+    """rt_set_max_paths: a budget larger than HBM (1024 frames of 1080p = 458 GB) runs fewer
+    frames per launch; the image equals a run with a small budget bit for bit."""
+    from rtamd.renderer import Renderer
+    sd = cf.config_scene("C2")
+    W, H = 1920, 1080
+    fp = cf.frame_params(W, H, max_bounce=1)
+    ro = cf.rand_origins(1024)
+    out = []
+    for budget in (1 << 40, 48 * W * H):
+        r = Renderer(0)
+        try:
+            r.set_scene_soa(sd.soa, sd.nodes)
+            r.set_env(env_maps[0], env_maps[1])
+            r.resize(W, H)
+            r.set_max_paths(budget)
+            r.render(fp, ro)
+            out.append(r.read_accum())
+        finally:
+            r.close()
+    assert bit_mismatch(out[0], out[1])[0] == 0.0
