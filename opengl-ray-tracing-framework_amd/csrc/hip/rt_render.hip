@@ -88,6 +88,7 @@ struct rt_ctx {
   rtd::WFState wfg[MAX_GROUPS]{};
   hipStream_t aux[MAX_GROUPS] = {};
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
+  float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera)
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
   size_t max_slots_req = 0;        // rt_set_max_paths (0: RT_MAX_SLOTS or the 320 Mi default)
@@ -313,26 +314,38 @@ int occupancy(rt_ctx* c) {
   if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode0 = c->trace_mode = std::max(0, std::min(3, atoi(e)));
   if (const char* e = getenv("RT_TRACE_MODE0")) c->trace_mode0 = std::max(0, std::min(3, atoi(e)));
   // persistent grids: as many blocks as can be resident, per schedule (their register counts differ)
-  auto occ = [&](int mode) {
+  auto occ = [&](int mode, bool cam) {
     int b = 0;
     hipError_t e;
-    switch (mode) {
-      case rtd::TM_IFIF:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true>, 256, c->trace_lds);
+    switch (mode * 2 + (cam ? 1 : 0)) {
+      case rtd::TM_IFIF * 2:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true, false>, 256, c->trace_lds);
         break;
-      case rtd::TM_WW:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true>, 256, c->trace_lds);
+      case rtd::TM_IFIF * 2 + 1:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true, true>, 256, c->trace_lds);
         break;
-      case rtd::TM_DUAL:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true>, 256, c->trace_lds);
+      case rtd::TM_WW * 2:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true, false>, 256, c->trace_lds);
+        break;
+      case rtd::TM_WW * 2 + 1:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true, true>, 256, c->trace_lds);
+        break;
+      case rtd::TM_DUAL * 2:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true, false>, 256, c->trace_lds);
+        break;
+      case rtd::TM_DUAL * 2 + 1:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true, true>, 256, c->trace_lds);
+        break;
+      case rtd::TM_SPEC * 2:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, false>, 256, c->trace_lds);
         break;
       default:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256, c->trace_lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, true>, 256, c->trace_lds);
     }
     return e == hipSuccess ? std::max(1, b) : 1;
   };
-  c->trace_bpc0 = occ(c->trace_mode0);
-  c->trace_bpc = occ(c->trace_mode);
+  c->trace_bpc0 = occ(c->trace_mode0, true);  // pass 0 is the implicit camera pass
+  c->trace_bpc = occ(c->trace_mode, false);
   bpc = c->trace_bpc;
   if (const char* e = getenv("RT_TRACE_BPC")) c->trace_bpc0 = c->trace_bpc = std::max(1, atoi(e));
   if (const char* e = getenv("RT_POOL_CHUNK")) c->pool_chunk = std::max(64, atoi(e) / 64 * 64);
@@ -341,7 +354,7 @@ int occupancy(rt_ctx* c) {
             "megakernel %d\n", kl, c->trace_lds, bpc, c->trace_bpc, c->trace_bpc0, c->blocks_per_cu);
     for (int l = 0; l <= 40960; l += 8192) {
       int b = 0;
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true>, 256, l);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, true>, 256, l);
       fprintf(stderr, "[rt]   occupancy(lds=%d) = %d\n", l, b);
     }
   }
@@ -358,19 +371,19 @@ int occupancy(rt_ctx* c) {
 
 template <bool COUNT, bool WIDE>
 void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
-  switch (WP.pass == 0 ? c->trace_mode0 : c->trace_mode) {
-    case rtd::TM_IFIF:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_IFIF, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
-      break;
-    case rtd::TM_WW:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_WW, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
-      break;
-    case rtd::TM_DUAL:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_DUAL, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
-      break;
-    default:
-      hipLaunchKernelGGL((rtd::wf_trace<COUNT, rtd::TM_SPEC, WIDE>), grid, dim3(256), c->trace_lds, st, WP);
+  const int mode = WP.pass == 0 ? c->trace_mode0 : c->trace_mode;
+#define RT_LAUNCH_TRACE(M)                                                                                  \
+  if (WP.cam_n)                                                                                           \
+    hipLaunchKernelGGL((rtd::wf_trace<COUNT, M, WIDE, true>), grid, dim3(256), c->trace_lds, st, WP);      \
+  else                                                                                                    \
+    hipLaunchKernelGGL((rtd::wf_trace<COUNT, M, WIDE, false>), grid, dim3(256), c->trace_lds, st, WP);
+  switch (mode) {
+    case rtd::TM_IFIF: RT_LAUNCH_TRACE(rtd::TM_IFIF) break;
+    case rtd::TM_WW: RT_LAUNCH_TRACE(rtd::TM_WW) break;
+    case rtd::TM_DUAL: RT_LAUNCH_TRACE(rtd::TM_DUAL) break;
+    default: RT_LAUNCH_TRACE(rtd::TM_SPEC)
   }
+#undef RT_LAUNCH_TRACE
 }
 
 template <bool COUNT>
@@ -490,6 +503,7 @@ int rt_destroy(rt_ctx* c) {
   if (c->h_ftab) (void)hipHostFree(c->h_ftab);
   dfree(c->d_ftab);
   dfree(c->d_pix);
+  dfree(c->d_cam);
   dfree(c->d_stack_ovf);
   dfree(c->d_disp);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -745,8 +759,10 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
   c->n_valid = (int)xy.size();
   dfree(c->d_pix);
+  dfree(c->d_cam);
   const size_t nv = std::max<size_t>(1, xy.size());
   HIPCHK(c, hipMalloc(&c->d_pix, 2 * nv * sizeof(unsigned int)));
+  HIPCHK(c, hipMalloc(&c->d_cam, nv * sizeof(float4)));
   if (!xy.empty()) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
@@ -756,6 +772,7 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   if (rc) return rc;
   c->wf.pix_xy = c->d_pix;
   c->wf.pix_acc = c->d_pix + nv;
+  c->wf.cam = c->d_cam;
   c->frame_set = true;
   c->loop_num = 0;
   return RT_OK;
@@ -912,11 +929,17 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.S = c->wfg[g];
         WP.S.pix_xy = c->wf.pix_xy;
         WP.S.pix_acc = c->wf.pix_acc;
+        WP.S.cam = c->wf.cam;
         WP.n_frames = f1 - f0;
         WP.pass = 0;
+        WP.cam_n = 0u;
         slots_g[g] = (unsigned)(f1 - f0) * (unsigned)c->n_valid;
         sg[g] = g == 0 ? c->stream : c->aux[g];
       }
+      // camera directions of this call's frames (every group reads them)
+      hipLaunchKernelGGL(rtd::wf_camera, dim3(std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256))),
+                         dim3(256), 0, c->stream, WG[0]);
+      HIPCHK(c, hipGetLastError());
       // aux streams start after everything already queued on the caller's stream
       if (G > 1) {
         hipEvent_t es = take_event(c);
@@ -943,7 +966,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         const int stages = std::max(1, std::min(c->stages, nfg));
         for (int pass = 0; pass <= last_pass + stages - 1; pass++) {
           WP.pass = pass;
-          if (pass < stages) {
+          // one stage: pass 0's camera paths are implicit (wf_trace / wf_shade generate them)
+          WP.cam_n = (stages == 1 && pass == 0) ? slots_g[g] : 0u;
+          if (pass < stages && stages > 1) {
             WP.gen_f0 = pass * nfg / stages;
             WP.gen_f1 = (pass + 1) * nfg / stages;
             const unsigned int runs = ((unsigned)(WP.gen_f1 - WP.gen_f0) * (unsigned)c->n_valid + rtd::GEN_RUN - 1) / rtd::GEN_RUN;

@@ -51,6 +51,7 @@ struct WFState {
   float4* __restrict__ fin;  // per path: final radiance curColor (RT:1549) awaiting the blend
   const unsigned int* __restrict__ pix_xy;   // per work item: px | py << 16
   const unsigned int* __restrict__ pix_acc;  // per work item: accumulation index
+  float4* __restrict__ cam;                   // per work item: camera direction, u * v (wf_camera)
   int* queue[2];                // ray queue entries: path << 1 | is_shadow
   int* active[2];               // active path ids
   unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
@@ -62,6 +63,10 @@ struct WFParams {
   int n_frames;  // frames in flight: slots = n_frames * K.n_work
   int pass;      // bounce pass: queue/active set pass&1 in, (pass+1)&1 out
   int gen_f0, gen_f1;  // wf_gen: the frames [gen_f0, gen_f1) whose camera paths start this pass
+  // implicit camera pass: when nonzero, this pass's ray queue and active list are the camera
+  // paths of slots [0, cam_n) in slot order (entry i = slot i), generated where they are used
+  // (wf_trace refill, wf_shade) instead of being written by wf_gen and read back
+  unsigned int cam_n;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -108,6 +113,33 @@ RTD unsigned int wave_lds_append(unsigned int* lcount, unsigned int n) {
   return (unsigned int)__shfl((int)base, 0) + mine;
 }
 
+// Per work item of this rank: the camera ray direction and u*v of its pixel (RT:1520-1527),
+// written once per render call; every frame's camera ray of that pixel reads it.
+__global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
+  const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
+  const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
+  for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < P.n_work; w += gridDim.x * blockDim.x) {
+    const unsigned int xy = S.pix_xy[w];
+    const int px = (int)(xy & 0xffffu), py = (int)(xy >> 16);
+    const float u = ((float)px + 0.5f) / (float)P.W;  // TexCoords (vertex_shader.glsl)
+    const float v = ((float)py + 0.5f) / (float)P.H;
+    const f3 d = normalize(lbc + (u * 2.0f * P.half_w) * right + (v * 2.0f * P.half_h) * up);  // R6
+    S.cam[w] = make_float4(d.x, d.y, d.z, u * v);
+  }
+}
+
+// Camera ray of path slot `slot`: direction, seed (R5) and frame of the slot.
+RTD f3 camera_ray(const KParams& P, const WFState& S, unsigned int slot, uint32_t& wseed, uint32_t& frame) {
+  const unsigned int f = slot / P.n_work;
+  const float4 c = S.cam[slot - f * P.n_work];
+  wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * c.w);  // R5: rand_origin * 6.95857 * (u * v)
+  frame = f;
+  return xyz(c);
+}
+
 // ------------------------------------------------------------------------------- gen
 // Camera paths of frames [gen_f0, gen_f1) (RT:1520-1527), appended to the ray queue and active
 // list of this pass.  Frames start in stages (one stage per pass for the first passes): every
@@ -119,9 +151,6 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1;
-  const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
-  const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
-  const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
   const unsigned int s0 = (unsigned)W.gen_f0 * P.n_work, s1 = (unsigned)W.gen_f1 * P.n_work;
   __shared__ unsigned int qbase, abase;
   for (unsigned int run = s0 + blockIdx.x * GEN_RUN; run < s1; run += gridDim.x * GEN_RUN) {
@@ -134,14 +163,8 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
     __syncthreads();
     for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
       const unsigned int slot = run + j;
-      const unsigned int f = slot / P.n_work;
-      const unsigned int w = slot - f * P.n_work;
-      const unsigned int xy = S.pix_xy[w];
-      const int px = (int)(xy & 0xffffu), py = (int)(xy >> 16);
-      const float u = ((float)px + 0.5f) / (float)P.W;  // TexCoords (vertex_shader.glsl)
-      const float v = ((float)py + 0.5f) / (float)P.H;
-      const uint32_t wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * (u * v));  // R5
-      const f3 d = normalize(lbc + (u * 2.0f * P.half_w) * right + (v * 2.0f * P.half_h) * up);  // R6
+      uint32_t wseed, f;
+      const f3 d = camera_ray(P, S, slot, wseed, f);
       S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
       S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
       S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
@@ -411,14 +434,16 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
 #endif
-template <bool COUNT, int MODE, bool WIDE>
+// CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
+// passes' kernels carry none of its registers
+template <bool COUNT, int MODE, bool WIDE, bool CAM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == TM_DUAL ? RT_TRACE_WPE_DUAL : RT_TRACE_WPE)))
 void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int qin = W.pass & 1;
-  const unsigned int nq = S.cnt[qin];
+  const unsigned int nq = CAM ? W.cam_n : S.cnt[qin];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
     S.cnt[qin ^ 1] = 0u;
     S.cnt[2 + (qin ^ 1)] = 0u;
@@ -426,7 +451,7 @@ void wf_trace(const WFParams W) {
   if (nq == 0u || !P.has_scene) {
     if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
       for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
-        int e = S.queue[qin][i];
+        const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
         S.res[e] = make_int2(-1, 0);
       }
     }
@@ -493,13 +518,22 @@ void wf_trace(const WFParams W) {
         const unsigned int rank = (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
         if (!busy && rank < avail) {
           const unsigned int slot = pool_next + rank;
-          entry = S.queue[qin][slot];
-          const int path = entry >> 1;
-          L.anyhit = (entry & 1) != 0;
-          const float4 oo = L.anyhit ? S.so[path] : S.ro[path];
-          const float4 dd = L.anyhit ? S.sd[path] : S.rd[path];
-          L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
-          L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+          if (CAM) {  // implicit camera pass: queue entry i is slot i's camera ray
+            entry = (int)(slot << 1);
+            L.anyhit = false;
+            uint32_t seed_unused, frame_unused;
+            const f3 d = camera_ray(P, S, slot, seed_unused, frame_unused);
+            L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
+            L.dx = d.x; L.dy = d.y; L.dz = d.z;
+          } else {
+            entry = S.queue[qin][slot];
+            const int path = entry >> 1;
+            L.anyhit = (entry & 1) != 0;
+            const float4 oo = L.anyhit ? S.so[path] : S.ro[path];
+            const float4 dd = L.anyhit ? S.sd[path] : S.rd[path];
+            L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
+            L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+          }
           L.ix = 1.0f / L.dx; L.iy = 1.0f / L.dy; L.iz = 1.0f / L.dz;
           // finite 1/d: per axis (lo-o)*inv <= (hi-o)*inv exactly when inv > 0 (rounding is
           // monotone), so the slab min/max of RT:309-310 is a fixed choice of plane per ray
@@ -669,9 +703,6 @@ void wf_trace(const WFParams W) {
 #ifndef RT_SH_SUB
 #define RT_SH_SUB 4
 #endif
-#ifndef RT_SH_EARLY  // issue every path-state load before the flags arrive (+0.6%, tools/ab_proc.py)
-#define RT_SH_EARLY 1
-#endif
 #ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0: +1.0%)
 #define RT_SH_KEY_MAT 0
 #endif
@@ -714,8 +745,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
-  const unsigned int na = S.cnt[2 + in];
-  const unsigned int nq_in = S.cnt[in];
+  const unsigned int na = W.cam_n ? W.cam_n : S.cnt[2 + in];
+  const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
   if (blockIdx.x == 0 && threadIdx.x == 0) S.cnt[4] = 0u;  // fetch counter of the next trace pass
   const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
@@ -737,7 +768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #pragma unroll
     for (int sub = 0; sub < SH_SUB; sub++) {
       const unsigned int j = (unsigned)sub * 256u + threadIdx.x;
-      if (j < nblk) lsort[j] = S.active[in][base + j];
+      if (j < nblk) lsort[j] = W.cam_n ? (int)(base + j) : S.active[in][base + j];
     }
   } else {
   int skey[SH_SUB], srank[SH_SUB], spath[SH_SUB];
@@ -779,8 +810,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     float hDist = 0.0f;
     int mat = 0;
     if (live) {
-      a5 = S.s5[path];
-#if RT_SH_EARLY
+      float4 cam_d = make_float4(0, 0, 0, 0);
+      if (W.cam_n) {  // implicit camera pass: the state wf_gen would have written
+        uint32_t cseed, cframe;
+        const f3 d = camera_ray(P, S, (unsigned)path, cseed, cframe);
+        a5 = make_uint4(cseed, 0u, PF_CONT | PF_CAMERA, cframe);
+        cam_d = make_float4(d.x, d.y, d.z, 0.0f);
+      } else {
+        a5 = S.s5[path];
+      }
       // every load of the path's state issues at once: camera paths exist only in pass 0 (a
       // uniform test), so no load waits for the flags; the flags still decide what is used
       int2 rsh = make_int2(0, 0);
@@ -789,21 +827,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         rsh = S.res[2 * path + 1];
       }
       const int2 rc0 = S.res[2 * path];
-      const float4 oo0 = S.ro[path], dd0 = S.rd[path];
-#endif
+      const float4 oo0 = W.cam_n ? make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f) : S.ro[path];
+      const float4 dd0 = W.cam_n ? cam_d : S.rd[path];
       wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
       if (!(flags & PF_CAMERA)) {
-#if !RT_SH_EARLY
-        a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path];
-#endif
         hist = xyz(a0); evp = a0.w;
         Lo = xyz(a1);
         evf = xyz(a2);
         Le0 = mk3(a1.w, a2.w, 0.0f);
-#if !RT_SH_EARLY
-        a3 = S.s3[path];
-        const int2 rsh = S.res[2 * path + 1];
-#endif
         Le0.z = a3.w;
         // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
         if ((flags & PF_SHADOW) && rsh.x < 0) Lo = Lo + xyz(a3);
@@ -817,13 +848,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         fin = Le0 + Lo;
         doFinish = true;
       } else {
-#if RT_SH_EARLY
         const int2 r = rc0;
         const float4 oo = oo0, dd = dd0;
-#else
-        const int2 r = S.res[2 * path];
-        const float4 oo = S.ro[path], dd = S.rd[path];
-#endif
         const f3 ro = xyz(oo), rd = xyz(dd);
         if (r.x >= 0) {
           const int tri = r.x;

@@ -8,9 +8,11 @@ groups, cur = [], None
 for r in rows:
     n = r["Kernel_Name"]
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    if "wf_gen" in n:
-        cur = {"gen": d, "trace": [], "shade": [], "blend": 0.0}
+    if "wf_camera" in n or ("wf_gen" in n and (cur is None or cur["blend"] or cur["trace"])):
+        cur = {"gen": d, "trace": [], "shade": [], "blend": 0.0}  # gen: wf_camera (+ wf_gen)
         groups.append(cur)
+    elif "wf_gen" in n:
+        cur["gen"] += d
     elif cur is not None:
         if "wf_trace" in n:
             cur["trace"].append(d)
