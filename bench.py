@@ -3,11 +3,13 @@
 
 Workload (default): config C3 = floor + loong_100000 (copper), 1920x1080, maxBounce 8,
 HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs.py).
-One *step* = ``--frames-per-step`` (default 512) progressive frames (1 spp each) of the whole
-frame, rendered by one rt_render call per rank over that rank's pixel tiles (frames in flight
-all in flight at once (rt_set_max_paths: 216 B per pixel-frame, 229 GB of HBM3E on one GPU,
-29 GB per rank on 8 tile-sharded GPUs), so every rank keeps plenty of work in flight: strong scaling of a fixed
-frame budget without a per-rank latency floor penalty), followed by the
+One *step* = ``--frames-per-step`` (default 1024 = the C3 config's spp)
+progressive frames (1 spp each) of the whole frame, rendered by one rt_render call per rank
+over that rank's pixel tiles with as many frames in flight as HBM holds (rt_set_max_paths:
+216 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 229 GB of path
+state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 57 GB per rank), so
+every rank keeps plenty of work in flight: strong scaling of a fixed frame budget without a
+per-rank latency-floor penalty (tools/rank_sim.py), followed by the
 frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
 torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
 
@@ -47,7 +49,7 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--frames-per-step", type=int, default=512)
+    ap.add_argument("--frames-per-step", type=int, default=1024)
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
@@ -129,9 +131,9 @@ def main() -> int:
     r.resize(W, H, tile=args.tile, rank=rank, world=world)
     info = r.device_info()
     ad = r.accum_device()
-    # path-state budget: a whole step's frames in flight at once (216 B per pixel-frame: 229 GB
-    # of HBM3E for 512 frames of 1080p on one GPU, 29 GB per rank at N = 8); the library runs
-    # fewer at a time if they do not fit
+    # path-state budget: a whole step's frames in flight at once (216 B per pixel-frame: 57 GB
+    # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
+    # until the state fits (512 = 229 GB of HBM3E on one GPU)
     path_slots = F * ad["local_tiles"] * args.tile * args.tile
     r.set_max_paths(path_slots)
     nfloat = ad["bytes"] // 4

@@ -26,6 +26,7 @@ ap.add_argument("--frames", type=int, default=512)
 ap.add_argument("--reps", type=int, default=2, help="timed render calls per measurement")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--one", default=None)
+ap.add_argument("--whole", action="store_true", help="path budget = frames x pixels (bench.py's setting)")
 a = ap.parse_args()
 
 if a.one is not None:
@@ -38,6 +39,8 @@ if a.one is not None:
     r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(*cf.load_env())
     r.resize(W, H)
+    if a.whole:
+        r.set_max_paths(a.frames * W * H)
     fp = cf.frame_params(W, H)
     ro = cf.rand_origins(a.frames)
     r.render(fp, ro)
@@ -62,7 +65,7 @@ res = {n: [] for n, _, _ in specs}
 for rnd in range(a.rounds):
     for name, path, env in specs:
         p = subprocess.run([sys.executable, __file__, "--one", path, "--config", a.config, "--frames", str(a.frames),
-                            "--reps", str(a.reps)], env={**os.environ, **env}, capture_output=True, text=True,
+                            "--reps", str(a.reps)] + (["--whole"] if a.whole else []), env={**os.environ, **env}, capture_output=True, text=True,
                            timeout=300)
         if p.returncode != 0:
             print(p.stderr[-2000:], flush=True)

@@ -19,6 +19,7 @@ ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--max-bounce", type=int, default=8)
 ap.add_argument("--flags", type=int, default=0)
+ap.add_argument("--count-frames", type=int, default=1, help="frames of the visit-counting render")
 a = ap.parse_args()
 cfg = cf.CONFIGS[a.config]
 W, H = a.width or cfg.width, a.height or cfg.height
@@ -32,7 +33,7 @@ r.set_env(*env)
 r.resize(W, H)
 print("device", r.device_info(), flush=True)
 fp = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=a.flags)
-ro = cf.rand_origins(a.frames + 1 + 64)
+ro = cf.rand_origins(a.frames + 1 + max(64, a.count_frames))
 r.render(fp, ro[:1])
 r.reset_stats()
 t = time.time()
@@ -48,7 +49,7 @@ print(f"{a.config} {W}x{H} mb={a.max_bounce} flags={a.flags}: {ms:.2f} ms/frame 
       f"{st['rays']/st['kernel_ms']/1e3:.1f} Mrays/s, rays/frame {st['rays']/a.frames/1e6:.2f} M", flush=True)
 fpc = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=RT_FLAG_COUNT_VISITS | a.flags)
 r.reset_stats()
-r.render(fpc, ro[-1:])
+r.render(fpc, ro[-a.count_frames:])
 st = r.stats()
 print("visits per ray: internal %.1f leaf %.1f tri %.1f; trace loop iters/wave-pass avg %.0f max %d (%d launches)" % (
       st["internal_pops"] / st["rays"], st["leaf_pops"] / st["rays"], st["tri_tests"] / st["rays"],

@@ -9,7 +9,7 @@ timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.l
 tail -2 gpurun_out/pytest_gpu.log
 bash tools/profile_gpu.sh gpurun_out/prof || { echo "profile failed"; exit 1; }
 python3 tools/summarize_profile.py gpurun_out/prof $TAG \
-  '{"config": "C3", "width": 1920, "height": 1080, "frames_per_launch": 512, "path_slots_per_rank": 1069547520, "command": "bash tools/profile_gpu.sh (bench.py --steps 5 --warmup 1 --cpu-seconds 0)"}' > gpurun_out/summary.log || exit 1
+  '{"config": "C3", "width": 1920, "height": 1080, "frames_per_launch": 1024, "path_slots_per_rank": 2139095040, "command": "bash tools/profile_gpu.sh (bench.py --steps 5 --warmup 1 --cpu-seconds 0)"}' > gpurun_out/summary.log || exit 1
 timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 mkdir -p gpurun_out/profiles && cp profiles/${TAG}_* profiles/pmc_traffic_C3.json gpurun_out/profiles/
