@@ -992,7 +992,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
             HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
             fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
-                    "wave-iters max %llu ray-steps max %llu\n", g, pass, q[0], ms, h[2], h[3], h[4], h[5], h[6], h[7]);
+                    "wave-iters max %llu ray-steps max %llu\n", g, pass, (WP.cam_n ? WP.cam_n : q[0]), ms, h[2], h[3], h[4], h[5], h[6], h[7]);
             fprintf(stderr, "[rt]   lane utilisation: node phase %.3f (%llu iters)  tri phase %.3f (%llu iters)  busy at "
                     "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
                     h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
