@@ -168,6 +168,14 @@ int rt_copy_accum_device(rt_ctx* ctx, void* dst_device, size_t bytes);
 /* Un-permute `world` gathered accumulation buffers (rank-major, each rt_accum_device bytes) on
  * this ctx's device into a width*height*3 float frame (device pointer). */
 int rt_assemble_frame(rt_ctx* ctx, const void* gathered_device, int32_t world, void* frame_device);
+/* Single-process form of the frame-end gather (SURVEY §8(b) rt_gather, §8(e)): ctxs[r] renders
+ * rank r of a world of n (rt_resize tiling; one context per device, or several on one).  After
+ * the work queued on each context, its accumulation tiles are copied peer to peer (xGMI between
+ * GPUs) into ctxs[0]'s device, un-permuted there (rt_assemble_frame) and read back: full_rgb =
+ * width*height*3 floats, row 0 = bottom (RT_LAYOUT_FRAME).  Synchronous; errors land in
+ * rt_last_error(ctxs[0]).  One process per GPU uses rt_copy_accum_device + an RCCL gather +
+ * rt_assemble_frame instead (bench.py). */
+int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb);
 
 /* Display / screenshot — replaces the tone-mapping pass
  * (src/shaders/fragment_shader_tone_mapping.glsl:66-93, main.cpp:215-227) or the screen blit

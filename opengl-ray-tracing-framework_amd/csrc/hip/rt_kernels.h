@@ -35,6 +35,7 @@ struct KParams {
   int max_bounce, flags, n_frames;
   const int* __restrict__ loop_num;       // per frame of this launch (device table)
   const float* __restrict__ rand_origin;  // per frame of this launch (device table)
+  const float2* __restrict__ sobol;       // per frame of this launch: sobolVec2 of bounces 0..3 (wf_sobol)
   int W, H, tile_w, tile_h, tiles_x, rank, world;
   unsigned int n_work;
   const GNode* __restrict__ nodes;  // binary tree; GNode.ref.z = DFS rank of the first leaf on the right

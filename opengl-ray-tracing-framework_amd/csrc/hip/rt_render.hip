@@ -74,6 +74,8 @@ struct rt_ctx {
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
+  void* d_gather = nullptr;                   // rt_gather on rank 0: every rank's tiles, then the frame
+  size_t gather_bytes = 0;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
   void* wf_mem = nullptr;
@@ -506,6 +508,7 @@ int rt_destroy(rt_ctx* c) {
   dfree(c->d_cam);
   dfree(c->d_stack_ovf);
   dfree(c->d_disp);
+  dfree(c->d_gather);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -837,7 +840,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     dfree(c->d_ftab);
     const size_t cap = std::max<size_t>(1024, (size_t)n_frames);
     HIPCHK(c, hipHostMalloc((void**)&c->h_ftab, 2 * cap * sizeof(int)));
-    HIPCHK(c, hipMalloc((void**)&c->d_ftab, 2 * cap * sizeof(int)));
+    // device table: [cap] loop_num, [cap] rand_origin, then [cap][4] float2 Sobol pairs (wf_sobol)
+    HIPCHK(c, hipMalloc((void**)&c->d_ftab, 10 * cap * sizeof(int)));
     c->ftab_cap = cap;
   }
   if (!c->ftab_event) HIPCHK(c, hipEventCreateWithFlags(&c->ftab_event, hipEventDisableTiming));
@@ -858,6 +862,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   HIPCHK(c, hipEventRecord(c->ftab_event, c->stream));
   const int* d_loop = c->d_ftab;
   const float* d_ro = reinterpret_cast<const float*>(c->d_ftab + c->ftab_cap);
+  float2* d_sobol = reinterpret_cast<float2*>(c->d_ftab + 2 * c->ftab_cap);
+  if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
+    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, c->stream, d_loop, d_sobol, n_traced);
+    HIPCHK(c, hipGetLastError());
+  }
   int done = 0;
   while (done < n_traced) {
     KParams P;
@@ -866,6 +875,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     const int nf = std::min(cap, n_traced - done);
     P.loop_num = d_loop + done;
     P.rand_origin = d_ro + done;
+    P.sobol = d_sobol + 4 * (size_t)done;
     done += nf;
     memcpy(P.pos, fp->position, 12); memcpy(P.lbc, fp->left_bottom_corner, 12);
     memcpy(P.right, fp->right, 12); memcpy(P.up, fp->up, 12);
@@ -919,6 +929,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K = P;
         WP.K.loop_num = P.loop_num + f0;
         WP.K.rand_origin = P.rand_origin + f0;
+        WP.K.sobol = P.sobol + 4 * f0;
         WP.K.n_frames = f1 - f0;
         WP.K.n_work = (unsigned)c->n_valid;
         WP.K.lds_entries = c->trace_lds_entries;
@@ -1229,6 +1240,67 @@ int rt_assemble_frame(rt_ctx* c, const void* gathered, int32_t world, void* fram
                      c->H, c->tile_w, c->tile_h, c->tiles_x, world, std::max(1, c->max_local_tiles));
   HIPCHK(c, hipGetLastError());
   return RT_OK;
+}
+
+int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb) {
+  if (!ctxs || n <= 0 || !full_rgb || !ctxs[0]) return RT_ERR_ARG;
+  rt_ctx* c0 = ctxs[0];
+  for (int r = 0; r < n; r++) {
+    const rt_ctx* c = ctxs[r];
+    if (!c) return fail(c0, RT_ERR_ARG, "rt_gather: null context");
+    if (!c->frame_set) return fail(c0, RT_ERR_STATE, "rt_gather: rt_resize every context first");
+    if (c->rank != r || c->world != n) return fail(c0, RT_ERR_ARG, "rt_gather: ctxs[r] must render rank r of a world of n");
+    if (c->W != c0->W || c->H != c0->H || c->tile_w != c0->tile_w || c->tile_h != c0->tile_h ||
+        c->max_local_tiles != c0->max_local_tiles)
+      return fail(c0, RT_ERR_ARG, "rt_gather: contexts differ in frame size or tiling");
+  }
+  const size_t part = (size_t)std::max(1, c0->max_local_tiles) * c0->tile_w * c0->tile_h * sizeof(float4);
+  const size_t frame = (size_t)c0->W * c0->H * 3 * sizeof(float);
+  HIPCHK(c0, hipSetDevice(c0->device));
+  if (part * n + frame > c0->gather_bytes) {
+    dfree(c0->d_gather);
+    c0->gather_bytes = 0;
+    HIPCHK(c0, hipMalloc(&c0->d_gather, part * n + frame));
+    c0->gather_bytes = part * n + frame;
+  }
+  char* g = static_cast<char*>(c0->d_gather);
+  std::vector<std::pair<int, hipEvent_t>> done;  // (device, event) per rank, destroyed after the copy
+  auto cleanup = [&]() {
+    for (auto& e : done) { (void)hipSetDevice(e.first); (void)hipEventDestroy(e.second); }
+    (void)hipSetDevice(c0->device);
+  };
+  int rc = RT_OK;
+  for (int r = 0; r < n && rc == RT_OK; r++) {
+    const rt_ctx* c = ctxs[r];
+    hipEvent_t e = nullptr;
+    hipError_t he = hipSetDevice(c->device);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (he == hipSuccess) done.push_back({c->device, e});
+    if (he == hipSuccess) he = hipEventRecord(e, c->stream);  // after everything queued on rank r
+    if (he == hipSuccess) he = hipSetDevice(c0->device);
+    if (he == hipSuccess && c->device != c0->device) {  // direct xGMI copies where the link allows
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, c0->device, c->device) == hipSuccess && can) {
+        const hipError_t pe = hipDeviceEnablePeerAccess(c->device, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) he = pe;
+        (void)hipGetLastError();
+      }
+    }
+    if (he == hipSuccess) he = hipStreamWaitEvent(c0->stream, e, 0);
+    if (he == hipSuccess)
+      he = hipMemcpyPeerAsync(g + (size_t)r * part, c0->device, c->d_accum, c->device, part, c0->stream);
+    if (he != hipSuccess) rc = fail(c0, RT_ERR_HIP, std::string("rt_gather: ") + hipGetErrorString(he));
+  }
+  if (rc == RT_OK) rc = rt_assemble_frame(c0, g, n, g + (size_t)n * part);
+  if (rc == RT_OK) {
+    hipError_t he = hipMemcpyAsync(full_rgb, g + (size_t)n * part, frame, hipMemcpyDeviceToHost, c0->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c0->stream);
+    if (he != hipSuccess) rc = fail(c0, RT_ERR_HIP, std::string("rt_gather: ") + hipGetErrorString(he));
+  } else {
+    (void)hipStreamSynchronize(c0->stream);  // the events may still be waited on
+  }
+  cleanup();
+  return rc;
 }
 
 }  // extern "C"

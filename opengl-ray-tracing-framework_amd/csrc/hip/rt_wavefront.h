@@ -131,6 +131,28 @@ __global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
   }
 }
 
+#ifndef RT_SOBOL_TABLE
+#define RT_SOBOL_TABLE 1
+#endif
+// Per frame of a render call: sobolVec2(loopNum + 1, bounce) of RT:616-620 for bounces 0..3
+// (Sobol dims 0..7), so wf_shade reads one float2 instead of running two bit loops per bounce.
+__global__ __launch_bounds__(256) void wf_sobol(const int* __restrict__ loop_num, float2* __restrict__ out, int n_frames) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_frames * 4) return;
+  int g = loop_num[i >> 2] + 1;
+  g = g ^ (g >> 1);  // grayCode (RT:598-600)
+  const int b = i & 3;
+  out[i] = make_float2(sobol_gray(2 * b, g), sobol_gray(2 * b + 1, g));
+}
+RTD void sobol_pair(const KParams& P, uint32_t frame, uint32_t bounce, float& sx, float& sy) {
+  sx = sy = 0.0f;  // bounce >= 4 reads dims >= 8: outside the table (R8)
+  if (bounce < 4u) {
+    const float2 s = P.sobol[frame * 4u + bounce];
+    sx = s.x;
+    sy = s.y;
+  }
+}
+
 // Camera ray of path slot `slot`: direction, seed (R5) and frame of the slot.
 RTD f3 camera_ray(const KParams& P, const WFState& S, unsigned int slot, uint32_t& wseed, uint32_t& frame) {
   const unsigned int f = slot / P.n_work;
@@ -957,10 +979,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         qShadow = true;
         nflags |= PF_SHADOW;
       }
+      float sx, sy;
+#if RT_SOBOL_TABLE
+      sobol_pair(P, frame, bounce, sx, sy);
+#else
       int g = P.loop_num[frame] + 1;
       g = g ^ (g >> 1);
-      float sx = sobol_gray((int)bounce * 2, g);
-      float sy = sobol_gray((int)bounce * 2 + 1, g);
+      sx = sobol_gray((int)bounce * 2, g);
+      sy = sobol_gray((int)bounce * 2 + 1, g);
+#endif
       const float cu = rand_(wseed), cv = rand_(wseed);
       sx += cu;
       if (sx > 1) sx -= 1;
@@ -1013,10 +1040,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       shp_mid = clock64();
 #endif
       // BSDF sample (RT:1408-1474)
+      float sx, sy;
+#if RT_SOBOL_TABLE
+      sobol_pair(P, frame, bounce, sx, sy);
+#else
       int g = P.loop_num[frame] + 1;
       g = g ^ (g >> 1);
-      float sx = sobol_gray((int)bounce * 2, g);
-      float sy = sobol_gray((int)bounce * 2 + 1, g);
+      sx = sobol_gray((int)bounce * 2, g);
+      sy = sobol_gray((int)bounce * 2 + 1, g);
+#endif
       const float cu = rand_(wseed), cv = rand_(wseed);
       sx += cu;
       if (sx > 1) sx -= 1;

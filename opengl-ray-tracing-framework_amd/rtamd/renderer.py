@@ -33,7 +33,7 @@ ABI_SYMBOLS = (
     "rt_update_materials", "rt_set_env", "rt_resize", "rt_reset", "rt_set_loop_num", "rt_get_loop_num",
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
-    "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths",
+    "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -174,6 +174,7 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
     L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
     L.rt_set_max_paths.argtypes = [vp, C.c_uint64]
+    L.rt_gather.argtypes = [C.POINTER(vp), C.c_int32, _f32p]
     return L
 
 
@@ -347,6 +348,16 @@ class Renderer:
     def assemble_frame(self, gathered_ptr: int, world: int, frame_ptr: int) -> None:
         self._check(self._L.rt_assemble_frame(self._h, C.c_void_p(gathered_ptr), world, C.c_void_p(frame_ptr)),
                     "rt_assemble_frame")
+
+    @staticmethod
+    def gather(ranks: Sequence["Renderer"]) -> np.ndarray:
+        """rt_gather: the full (H, W, 3) frame (row 0 = bottom) from contexts ranks[r] = rank r of
+        len(ranks), assembled on ranks[0]'s device (single-process multi-GPU)."""
+        r0 = ranks[0]
+        hs = (C.c_void_p * len(ranks))(*[r._h.value for r in ranks])
+        out = np.zeros((r0.height, r0.width, 3), np.float32)
+        r0._check(r0._L.rt_gather(hs, len(ranks), _fp(out)), "rt_gather")
+        return out
 
     def tonemap(self, flags: int = RT_DISPLAY_TONEMAP | RT_DISPLAY_GAMMA, frame_ptr: Optional[int] = None) -> np.ndarray:
         """The displayed 8-bit image (H, W, 3), row 0 = top: the tone-mapping pass / screen blit +

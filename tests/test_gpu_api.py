@@ -151,6 +151,34 @@ def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
     assert bit_mismatch(host[..., :3], ref)[0] == 0.0
 
 
+def test_single_process_gather(gpu_renderer, env_maps):
+    """rt_gather: three rank contexts (one device here; peer copies between GPUs on a node)
+    render their tiles asynchronously; the gathered frame equals the oracle bit for bit, and a
+    context that is not rank r of the world is refused."""
+    from rtamd.renderer import Renderer
+    sd = cf.config_scene("C2")
+    W, H, T, world = 72, 40, 16, 3
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 3)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    ctxs = [gpu_renderer] + [Renderer(0) for _ in range(world - 1)]
+    try:
+        for rank, r in enumerate(ctxs):
+            r.set_scene_soa(sd.soa, sd.nodes)
+            r.set_env(env_maps[0], env_maps[1])
+            r.resize(W, H, tile=T, rank=rank, world=world)
+            r.set_loop_num(0)
+            r.clear_accum()
+            r.render_async(fp, ro)  # no synchronisation: rt_gather orders the copies itself
+        img = Renderer.gather(ctxs)
+        with pytest.raises(RuntimeError, match="rank r"):
+            Renderer.gather([ctxs[1], ctxs[0], ctxs[2]])
+    finally:
+        for r in ctxs[1:]:
+            r.close()
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
 def test_path_budget_beyond_device_memory_falls_back(env_maps):
     """rt_set_max_paths: a budget larger than HBM (1024 frames of 1080p = 458 GB) runs fewer
     frames per launch; the image equals a run with a small budget bit for bit."""
