@@ -136,6 +136,107 @@ void pack_material(const rt_material& m, float* o) {
   o[27] = o[28] = o[29] = o[30] = o[31] = 0.0f;
 }
 
+// New internal levels over the reference's leaves.  A leaf keeps its triangle range and its exact
+// box (the reference's, RT:363-368); every internal box is the exact min/max union of the boxes
+// below it.  The slab arithmetic is monotone in the box planes, so a box can only be hit when
+// every box above it is: the traversal reaches exactly the leaves whose own box the reference's
+// ray hits, whatever the internal levels are (the reference's exact-tie order is kept separately,
+// by the leaf ranks of its own tree).  The reference's top levels are X-median splits (R18: SAH
+// costs above INF = 114514 fall back to the median), so a full-sweep SAH over the leaf boxes
+// (centroid order per axis, cost = area x triangles) gives a tree with fewer node visits.
+// Returns the root of `out` (binary GNodes, host only: the device keeps the reference tree).
+int rebuild_over_leaves(const std::vector<GNode>& gn, int root, std::vector<GNode>& out) {
+  struct Box {
+    float lo[3], hi[3];
+  };
+  struct Prim {
+    int ref, n;
+    Box b;
+    double c[3];
+  };
+  auto is_leaf = [](int r) { return ((uint32_t)r & rtd::LEAF_BIT) != 0u; };
+  std::vector<Prim> prims;
+  std::vector<int> st{root};
+  while (!st.empty()) {
+    const GNode g = gn[st.back()];
+    st.pop_back();
+    const Box bl = {{g.b0.x, g.b0.y, g.b0.z}, {g.b0.w, g.b1.x, g.b1.y}};
+    const Box br = {{g.b1.z, g.b1.w, g.b2.x}, {g.b2.y, g.b2.z, g.b2.w}};
+    const int refs[2] = {g.ref.x, g.ref.y};
+    const Box* boxes[2] = {&bl, &br};
+    for (int k = 0; k < 2; k++) {
+      if (!is_leaf(refs[k])) { st.push_back(refs[k]); continue; }
+      Prim p;
+      p.ref = refs[k];
+      p.n = (int)((uint32_t)refs[k] & 15u) + 1;      p.b = *boxes[k];
+      for (int a = 0; a < 3; a++) p.c[a] = 0.5 * ((double)p.b.lo[a] + (double)p.b.hi[a]);
+      prims.push_back(p);
+    }
+  }
+  auto unite = [](const Box& a, const Box& b) {
+    Box u;
+    for (int k = 0; k < 3; k++) { u.lo[k] = std::min(a.lo[k], b.lo[k]); u.hi[k] = std::max(a.hi[k], b.hi[k]); }
+    return u;
+  };
+  auto area = [](const Box& b) {
+    double e[3];
+    for (int k = 0; k < 3; k++) e[k] = std::max(0.0, (double)b.hi[k] - (double)b.lo[k]);
+    return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+  };
+  std::vector<int> idx(prims.size()), tmp(prims.size());
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = (int)i;
+  std::vector<double> right_cost(prims.size() + 1);
+  out.clear();
+  out.reserve(prims.size());
+  std::function<int(int, int, Box&)> rec = [&](int b, int e, Box& box) -> int {
+    if (e - b == 1) {
+      box = prims[idx[b]].b;
+      return prims[idx[b]].ref;
+    }
+    double best = 1e300;
+    int bax = 0, bpos = b + (e - b) / 2;
+    for (int ax = 0; ax < 3; ax++) {
+      std::copy(idx.begin() + b, idx.begin() + e, tmp.begin() + b);
+      std::sort(tmp.begin() + b, tmp.begin() + e, [&](int x, int y) {
+        return prims[x].c[ax] < prims[y].c[ax] || (prims[x].c[ax] == prims[y].c[ax] && x < y);
+      });
+      Box acc = prims[tmp[e - 1]].b;
+      int cnt = 0;
+      for (int i = e - 1; i > b; i--) {  // right_cost[i] = cost of [i, e)
+        acc = unite(acc, prims[tmp[i]].b);
+        cnt += prims[tmp[i]].n;
+        right_cost[i - b] = area(acc) * cnt;
+      }
+      acc = prims[tmp[b]].b;
+      cnt = 0;
+      for (int i = b; i < e - 1; i++) {  // split after i: [b, i] | [i + 1, e)
+        acc = unite(acc, prims[tmp[i]].b);
+        cnt += prims[tmp[i]].n;
+        const double c = area(acc) * cnt + right_cost[i + 1 - b];
+        if (c < best) { best = c; bax = ax; bpos = i + 1; }
+      }
+    }
+    std::sort(idx.begin() + b, idx.begin() + e, [&](int x, int y) {
+      return prims[x].c[bax] < prims[y].c[bax] || (prims[x].c[bax] == prims[y].c[bax] && x < y);
+    });
+    const int me = (int)out.size();
+    out.push_back(GNode{});
+    Box lb, rb;
+    const int lr = rec(b, bpos, lb), rr = rec(bpos, e, rb);
+    GNode g;
+    memset(&g, 0, sizeof(g));
+    g.b0 = make_float4(lb.lo[0], lb.lo[1], lb.lo[2], lb.hi[0]);
+    g.b1 = make_float4(lb.hi[1], lb.hi[2], rb.lo[0], rb.lo[1]);
+    g.b2 = make_float4(rb.lo[2], rb.hi[0], rb.hi[1], rb.hi[2]);
+    g.ref = make_int4(lr, rr, 0, 0);
+    out[me] = g;
+    box = unite(lb, rb);
+    return me;
+  };
+  Box rootbox;
+  return rec(0, (int)prims.size(), rootbox);
+}
+
 // Leaf ranks + 4-wide collapse of the binary tree.
 // * Leaf rank = position of the leaf in the reference's left-first DFS; gn[k].ref.z = rank of
 //   the first leaf of node k's right subtree; trin[3t+1].w = rank of triangle t's leaf.  These
@@ -174,12 +275,22 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     trin[3 * t + 1].w = w;
   }
   if (!ok) return false;
+  // The tree that gets collapsed: by default internal levels rebuilt over the reference's leaves
+  // (rebuild_over_leaves), RT_REBUILD=0 keeps the reference's own internal nodes.
+  std::vector<GNode> rebuilt;
+  int croot = root;
+  const std::vector<GNode>* T = &gn;
+  const char* re = getenv("RT_REBUILD");
+  if (!is_leaf(root) && !(re && atoi(re) == 0)) {
+    croot = rebuild_over_leaves(gn, root, rebuilt);
+    T = &rebuilt;
+  }
   struct Slot {
     int ref;
     float lo[3], hi[3];
   };
   auto kids = [&](int b, Slot& L, Slot& R) {
-    const GNode& g = gn[b];
+    const GNode& g = (*T)[b];
     L = Slot{g.ref.x, {g.b0.x, g.b0.y, g.b0.z}, {g.b0.w, g.b1.x, g.b1.y}};
     R = Slot{g.ref.y, {g.b1.z, g.b1.w, g.b2.x}, {g.b2.y, g.b2.z, g.b2.w}};
   };
@@ -195,11 +306,11 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
   // RT_COLLAPSE=greedy: open the largest-area internal slot until there are four.
   const char* ce = getenv("RT_COLLAPSE");
   const bool greedy = ce && strcmp(ce, "greedy") == 0;
-  const size_t nb = gn.size();
+  const size_t nb = T->size();
   std::vector<double> f(nb * 5, 0.0);
   std::vector<signed char> split(nb * 5, 0);  // 0: keep the node as one slot, j > 0: j slots to the left
   auto fr = [&](int r, int k) -> double { return is_leaf(r) ? 0.0 : f[(size_t)r * 5 + k]; };
-  if (!greedy && !is_leaf(root)) {
+  if (!greedy && !is_leaf(croot)) {
     std::function<void(int)> dp = [&](int b) {
       Slot L, R;
       kids(b, L, R);
@@ -226,7 +337,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
         split[(size_t)b * 5 + k] = (signed char)bj;
       }
     };
-    dp(root);
+    dp(croot);
   }
   // DP reconstruction: the slots that binary subtree s contributes when given k of them
   std::function<void(const Slot&, int, std::vector<Slot>&)> collect = [&](const Slot& s, int k, std::vector<Slot>& out) {
@@ -284,7 +395,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     q.pad = make_int4((int)sl.size(), 0, 0, 0);
     return idx;
   };
-  qroot = is_leaf(root) ? root : build(root, 1);
+  qroot = is_leaf(croot) ? croot : build(croot, 1);
   return true;
 }
 
