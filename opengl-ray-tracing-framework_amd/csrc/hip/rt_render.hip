@@ -69,7 +69,7 @@ struct rt_ctx {
   hipEvent_t ftab_event = nullptr;            // the last upload (the host table is reused after it)
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
-  int pool_chunk = 256;                       // rays per queue atomic in wf_trace
+  int pool_chunk = 512;                       // rays per queue atomic in wf_trace (C3: 256 -> 512 +2.3%)
   int stagger = -1;                           // >= 0: group g starts after group g-1's pass `stagger` (measured slower)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)

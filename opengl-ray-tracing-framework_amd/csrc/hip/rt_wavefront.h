@@ -450,8 +450,9 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 1
 #endif
-#ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s
-#define RT_REFILL_MIN 16
+#ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s;
+                       // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%
+#define RT_REFILL_MIN 24
 #endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
