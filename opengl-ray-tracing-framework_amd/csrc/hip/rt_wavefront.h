@@ -722,9 +722,9 @@ void wf_trace(const WFParams W) {
 
 // ----------------------------------------------------------------------------- shade
 // Paths per block-iteration of wf_shade = 256 x SH_SUB: the block stages its queue / active
-// entries in LDS and claims global space with one atomic per list per 1024 paths.
-#ifndef RT_SH_SUB
-#define RT_SH_SUB 4
+// entries in LDS and claims global space with one atomic per list per block-iteration.
+#ifndef RT_SH_SUB  // C3 on the rebuilt tree: 1 / 2 / 4 / 8 -> -1.2% / 0 / -0.9% / -1.4% (tools/ab_proc.py)
+#define RT_SH_SUB 2
 #endif
 #ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0: +1.0%)
 #define RT_SH_KEY_MAT 0
