@@ -1144,7 +1144,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           }
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
-          hipLaunchKernelGGL(rtd::wf_shade, dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          if (fp->enable_bsdf)
+            hipLaunchKernelGGL(rtd::wf_shade<true>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          else
+            hipLaunchKernelGGL(rtd::wf_shade<false>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
           HIPCHK(c, hipGetLastError());
           if (g + 1 < G && pass == std::min(c->stagger, last_pass)) {
             prev_stagger = take_event(c);

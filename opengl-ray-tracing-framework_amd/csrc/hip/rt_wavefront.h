@@ -759,6 +759,9 @@ constexpr int SH_SUB = RT_SH_SUB;
 #define SHP_MARK(i)
 #endif
 
+// BSDF: enableBSDF (RT:1369 Disney integrator) or the BRDF integrator (RT:1290), one
+// instantiation each so neither carries the other's registers
+template <bool BSDF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
   __shared__ int lq[2 * 256 * SH_SUB];
   __shared__ int la[256 * SH_SUB];
@@ -895,7 +898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
             Lo = splat(0.0f);
             hist = splat(1.0f);
             bounce = 0;
-          } else if (P.enable_bsdf) {  // RT:1509-1510
+          } else if (BSDF) {  // RT:1509-1510
             const f3 Le = xyz(P.mats[8 * nmat]);
             Lo = Lo + hist * Le * evf / evp;
             bounce++;
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         } else if (flags & PF_CAMERA) {  // RT:1532-1539
           fin = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
           doFinish = true;
-        } else if (!P.enable_bsdf) {  // BRDF mode RT:1345-1359
+        } else if (!BSDF) {  // BRDF mode RT:1345-1359
           const float aNdotL = fabs_(S.s4[path].x);
           if (P.enable_env) {
             f3 skyColor;
@@ -958,7 +961,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     uint32_t nflags = 0;
     f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
     float bNdotL = 0.0f;  // BRDF mode: N.L of the sampled direction (RT:1336)
-    if (doBounce && !P.enable_bsdf) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
+    if (doBounce && !BSDF) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
       const Mat m = load_mat(P.mats, mat);
       const f3 V = -hV, N = hN;
       const float xa = rand_(wseed);
@@ -1121,7 +1124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
       S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
       if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
-      if (!P.enable_bsdf && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
+      if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
       S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
       if (qCont) {
         S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
