@@ -14,7 +14,7 @@
 //              (RT:1376-1474); finished paths blend into the accumulation (RT:1552)
 //
 // wf_trace + wf_shade repeat maxBounce+1 times; passes with no work exit at once.  All frames
-// of one launch are in flight together (path slot = frame * n_work + pixel): a pixel's frames
+// of one launch are in flight together (path slot = pixel * n_frames + frame): a pixel's frames
 // are independent until the progressive blend, so wf_blend applies RT:1552 afterwards in frame
 // order, exactly as sequential frames would.  This amortises the serial tail of the deepest
 // rays of each pass over several frames.  Shadow and continuation rays of all paths share one
@@ -153,10 +153,15 @@ RTD void sobol_pair(const KParams& P, uint32_t frame, uint32_t bounce, float& sx
   }
 }
 
-// Camera ray of path slot `slot`: direction, seed (R5) and frame of the slot.
+// Camera ray of path slot `slot`: direction, seed (R5) and frame of the slot.  Path slots are
+// pixel-major (slot = work item * n_frames + frame): the camera pass hands a wave one pixel's
+// frames, whose camera rays are the same ray (R6: no jitter), so its lanes traverse in lockstep,
+// and the next passes start from the same hit point.
 RTD f3 camera_ray(const KParams& P, const WFState& S, unsigned int slot, uint32_t& wseed, uint32_t& frame) {
-  const unsigned int f = slot / P.n_work;
-  const float4 c = S.cam[slot - f * P.n_work];
+  const unsigned int nf = (unsigned int)P.n_frames;
+  const unsigned int w = slot / nf;
+  const unsigned int f = slot - w * nf;
+  const float4 c = S.cam[w];
   wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * c.w);  // R5: rand_origin * 6.95857 * (u * v)
   frame = f;
   return xyz(c);
@@ -173,9 +178,11 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1;
-  const unsigned int s0 = (unsigned)W.gen_f0 * P.n_work, s1 = (unsigned)W.gen_f1 * P.n_work;
+  // item j of this stage = (work item j / nst, frame gen_f0 + j % nst): slots are pixel-major
+  const unsigned int nst = (unsigned)(W.gen_f1 - W.gen_f0), nfr = (unsigned)P.n_frames;
+  const unsigned int s1 = nst * P.n_work;
   __shared__ unsigned int qbase, abase;
-  for (unsigned int run = s0 + blockIdx.x * GEN_RUN; run < s1; run += gridDim.x * GEN_RUN) {
+  for (unsigned int run = blockIdx.x * GEN_RUN; run < s1; run += gridDim.x * GEN_RUN) {
     const unsigned int n = min(GEN_RUN, s1 - run);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -184,7 +191,8 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
     }
     __syncthreads();
     for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
-      const unsigned int slot = run + j;
+      const unsigned int item = run + j, w = item / nst;
+      const unsigned int slot = w * nfr + (unsigned)W.gen_f0 + (item - w * nst);
       uint32_t wseed, f;
       const f3 d = camera_ray(P, S, slot, wseed, f);
       S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
     const float4 h = P.accum[ai];
     f3 acc = mk3(h.x, h.y, h.z);
     for (int f = 0; f < W.n_frames; f++) {
-      const float4 c = S.fin[(size_t)f * P.n_work + w];
+      const float4 c = S.fin[(size_t)w * (unsigned)W.n_frames + (unsigned)f];
       const int loopNum = P.loop_num[f];
       const float n = (float)loopNum;
       acc = (1.0f / n) * xyz(c) + ((float)(loopNum - 1) / n) * acc;

@@ -1,0 +1,9 @@
+# pixel-major path slots: parity (incl. staged start), then A/B
+export TMPDIR=/tmp
+L=opengl-ray-tracing-framework_amd/lib/exp
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_api.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest16.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/pytest16.log; exit 1; }
+tail -1 gpurun_out/pytest16.log
+RT_STAGES=3 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest16s.log 2>&1 || { echo "staged gpu tests failed"; tail -30 gpurun_out/pytest16s.log; exit 1; }
+tail -1 gpurun_out/pytest16s.log
+timeout -k 10 900 python3 tools/ab_proc.py --whole --rounds 3 pm=default old=$L/librtamd_old.so > gpurun_out/ab16.log 2>&1 || { echo ab failed; tail -20 gpurun_out/ab16.log; exit 1; }
+tail -3 gpurun_out/ab16.log
