@@ -69,7 +69,7 @@ struct rt_ctx {
   hipEvent_t ftab_event = nullptr;            // the last upload (the host table is reused after it)
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
-  int pool_chunk = 512;                       // rays per queue atomic in wf_trace (C3: 256 -> 512 +2.3%)
+  int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
   int stagger = -1;                           // >= 0: group g starts after group g-1's pass `stagger` (measured slower)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
@@ -420,9 +420,10 @@ int occupancy(rt_ctx* c) {
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
   bpc = 0;
-  // measured per pass on C3: coherent camera rays prefer the speculative while-while schedule,
-  // incoherent secondary rays the dual-front one (tools/exp_dual2.sh)
-  c->trace_mode0 = rtd::TM_SPEC;
+  // measured per pass on C3: coherent camera rays preferred the speculative while-while schedule
+  // and incoherent secondary rays the dual-front one (tools/exp_dual2.sh); with pixel-major
+  // slots a camera-pass wave traces one ray 64 times and the dual schedule is as good (+0.3%)
+  c->trace_mode0 = rtd::TM_DUAL;
   c->trace_mode = rtd::TM_DUAL;
   if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode0 = c->trace_mode = std::max(0, std::min(3, atoi(e)));
   if (const char* e = getenv("RT_TRACE_MODE0")) c->trace_mode0 = std::max(0, std::min(3, atoi(e)));
