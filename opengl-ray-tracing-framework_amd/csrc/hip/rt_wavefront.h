@@ -738,8 +738,8 @@ void wf_trace(const WFParams W) {
 #define RT_SH_KEY_MAT 0
 #endif
 constexpr int SH_KEYS = 8;  // 0: no continuation hit; 1 + material id % 7: continuation hit
-#ifndef RT_SH_SORT_MIN
-#define RT_SH_SORT_MIN (1u << 24)
+#ifndef RT_SH_SORT_MIN  // C3, pixel-major slots: 4 / 16 / 32 / 64 / 128 / 256 Mi -> -1.6 / -1.4 / -0.5 / 0 / +0.1 / +0.2%
+#define RT_SH_SORT_MIN (1u << 26)
 #endif
 constexpr unsigned int SH_SORT_MIN = RT_SH_SORT_MIN;  // active paths from which wf_shade sorts
 
