@@ -462,6 +462,12 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
                        // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%
 #define RT_REFILL_MIN 24
 #endif
+#ifndef RT_TAIL_CHUNK  // rays per claim near the end of a pass queue (and per participating wave)
+#define RT_TAIL_CHUNK 64u
+#endif
+#ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
+#define RT_TAIL_FACTOR 4u
+#endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
 #endif
@@ -501,11 +507,11 @@ void wf_trace(const WFParams W) {
   bool busy = false;
   // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
   unsigned int pool_next = 0, pool_end = 0;
-  const unsigned int tail_rays = gridDim.x * TL_LANES * 4u;
+  const unsigned int tail_rays = gridDim.x * TL_LANES * RT_TAIL_FACTOR;
   // only as many waves as the queue can feed take part: every claim is an atomic on one word,
   // and thousands of empty-handed claims in a small late pass serialise at that address
   const unsigned int wave_id = blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6);
-  bool drained = wave_id >= (nq + 63u) / 64u;
+  bool drained = wave_id >= (nq + RT_TAIL_CHUNK - 1u) / RT_TAIL_CHUNK;
   const int lane = (int)(threadIdx.x & 63);
   int entry = 0, parked = 0;
   bool haveParked = false;
@@ -533,7 +539,7 @@ void wf_trace(const WFParams W) {
     // than the lanes it brings back
     if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
       if (pool_next >= pool_end) {
-        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : 64u;
+        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
