@@ -204,21 +204,41 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
   }
 }
 
-// progressive blend of the frames in flight, in frame order (RT:1552)
+// progressive blend of the frames in flight, in frame order (RT:1552).  Pixel-major slots put
+// a pixel's frames side by side, so the block stages 8 frames of its 256 pixels at a time in LDS
+// with whole-cache-line loads (8 lanes per pixel) and each thread then blends its own pixel.
+constexpr int BL_FR = 8, BL_PITCH = BL_FR + 1;  // frames per stage; padded row (bank spread)
 __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
+  __shared__ float4 tile[256 * BL_PITCH];
   const KParams& P = W.K;
   const WFState& S = W.S;
-  for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < P.n_work; w += gridDim.x * blockDim.x) {
-    const unsigned int ai = S.pix_acc[w];
-    const float4 h = P.accum[ai];
-    f3 acc = mk3(h.x, h.y, h.z);
-    for (int f = 0; f < W.n_frames; f++) {
-      const float4 c = S.fin[(size_t)w * (unsigned)W.n_frames + (unsigned)f];
-      const int loopNum = P.loop_num[f];
-      const float n = (float)loopNum;
-      acc = (1.0f / n) * xyz(c) + ((float)(loopNum - 1) / n) * acc;
+  const unsigned int nf = (unsigned int)W.n_frames;
+  for (unsigned int base = blockIdx.x * 256u; base < P.n_work; base += gridDim.x * 256u) {
+    const unsigned int w = base + threadIdx.x;
+    const bool valid = w < P.n_work;
+    const unsigned int ai = valid ? S.pix_acc[w] : 0u;
+    f3 acc = splat(0.0f);
+    if (valid) {
+      const float4 h = P.accum[ai];
+      acc = mk3(h.x, h.y, h.z);
     }
-    P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+    for (unsigned int f0 = 0; f0 < nf; f0 += BL_FR) {
+      const unsigned int nfc = min((unsigned int)BL_FR, nf - f0);
+      __syncthreads();
+      for (unsigned int i = threadIdx.x; i < 256u * BL_FR; i += 256u) {
+        const unsigned int p = i / BL_FR, k = i % BL_FR;
+        if (base + p < P.n_work && k < nfc) tile[p * BL_PITCH + k] = S.fin[(size_t)(base + p) * nf + f0 + k];
+      }
+      __syncthreads();
+      if (valid)
+        for (unsigned int k = 0; k < nfc; k++) {
+          const float4 c = tile[threadIdx.x * BL_PITCH + k];
+          const int loopNum = P.loop_num[f0 + k];
+          const float n = (float)loopNum;
+          acc = (1.0f / n) * xyz(c) + ((float)(loopNum - 1) / n) * acc;
+        }
+    }
+    if (valid) P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
   }
 }
 
