@@ -67,8 +67,9 @@ def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_m
     assert bit_mismatch(img3, ref)[0] == 0.0
 
 
-@pytest.mark.parametrize("width", ["4", "2"], ids=["bvh4", "bvh2"])
-def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monkeypatch, width):
+@pytest.mark.parametrize("width,rebuild", [("4", "1"), ("4", "0"), ("2", "1")],
+                         ids=["bvh4-rebuilt", "bvh4-reflevels", "bvh2"])
+def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monkeypatch, width, rebuild):
     """Two copies of the bunny at the same place with different materials: every hit on it is an
     exact distance tie between two triangles in different leaves.  The reference keeps the one
     its near-first DFS reaches first; the 4-wide traversal visits leaves in another order and
@@ -80,9 +81,30 @@ def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monk
     ro, frames = frames_for(fp, 1, 1)
     ref, cnt = oracle_render(sd, env_maps, W, H, frames)
     monkeypatch.setenv("RT_BVH_WIDTH", width)
+    monkeypatch.setenv("RT_REBUILD", rebuild)
     img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
     assert st["rays"] == cnt["rays"]
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("name", ["C3", "C5"])
+def test_reference_internal_levels_match_too(gpu_renderer, env_maps, monkeypatch, name):
+    """RT_REBUILD=0 collapses the reference's own internal nodes instead of the SAH levels rebuilt
+    over its leaves (rebuild_over_leaves): both reach exactly the leaves whose boxes the ray hits,
+    so both images equal the oracle, and the rebuilt tree takes fewer node steps per ray."""
+    from rtamd.renderer import RT_FLAG_COUNT_VISITS
+    sd = cf.config_scene(name)
+    W, H = 64, 36
+    fp = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS)
+    ro, frames = frames_for(fp, 1, 1)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    visits = {}
+    for rebuild in ("0", "1"):
+        monkeypatch.setenv("RT_REBUILD", rebuild)
+        img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+        assert bit_mismatch(img, ref)[0] == 0.0, rebuild
+        visits[rebuild] = st["internal_pops"] / st["rays"]
+    assert visits["1"] < visits["0"], visits
 
 
 def test_binary_wavefront_traversal_matches(gpu_renderer, env_maps, monkeypatch):
