@@ -108,7 +108,8 @@ RTD Mat load_mat(const float4* __restrict__ mats, int id) {
 
 // ------------------------------------------------------------------ env textures (R13)
 // texture() with NEAREST + CLAMP_TO_EDGE on W x H float4 texels.
-RTD float4 tex_nearest(const float4* __restrict__ img, int w, int h, float u, float v) {
+template <class T>
+RTD T tex_nearest(const T* __restrict__ img, int w, int h, float u, float v) {
   int i = (int)floor_(u * (float)w);
   int j = (int)floor_(v * (float)h);
   if (isnan_(u)) i = 0;
@@ -118,9 +119,12 @@ RTD float4 tex_nearest(const float4* __restrict__ img, int w, int h, float u, fl
   return img[(size_t)j * w + i];
 }
 
+// hdr texel = {hdrMap.rgb, hdrCache.b (pdf)}: hdrColor and hdrPdf of a direction read the same
+// texel of both maps (RT:1165-1186), so one 16-B fetch serves both; cache = hdrCache.rg, the
+// inverse-CDF sample of SampleHdr (RT:636).  Same values as the two RGB32F textures.
 struct Env {
   const float4* __restrict__ hdr;
-  const float4* __restrict__ cache;
+  const float2* __restrict__ cache;
   int w, h, res;
   float angle, intensity;
 };
@@ -136,7 +140,7 @@ RTD void toSphericalCoord(const Env& E, f3 v, float& u, float& w) {  // RT:625-6
   w = uy + 0.0f;
 }
 RTD f3 SampleHdr(const Env& E, float xi_1, float xi_2) {  // RT:635-646
-  float4 c = tex_nearest(E.cache, E.w, E.h, xi_1, xi_2);
+  float2 c = tex_nearest(E.cache, E.w, E.h, xi_1, xi_2);
   float x = c.x;
   float y = 1.0f - c.y;
   float phi = 2.0f * PI * (x - 0.5f);
@@ -154,7 +158,7 @@ RTD f3 hdrColor(const Env& E, f3 L) {  // RT:1165-1169
 RTD float hdrPdf(const Env& E, f3 L) {  // RT:1173-1186
   float u, v;
   toSphericalCoord(E, normalize(L), u, v);
-  float pdf = tex_nearest(E.cache, E.w, E.h, u, v).z;
+  float pdf = tex_nearest(E.hdr, E.w, E.h, u, v).w;
   float theta = PI * v;
   float sin_theta = max_(sin_(theta), 1e-10f);
   float p_convert = (float)(E.res * E.res / 2) / (TWO_PI * PI * sin_theta);
@@ -164,8 +168,9 @@ RTD float hdrPdf(const Env& E, f3 L) {  // RT:1173-1186
 RTD void hdrColorPdf(const Env& E, f3 L, f3& color, float& pdfv) {
   float u, v;
   toSphericalCoord(E, normalize(L), u, v);
-  color = xyz(tex_nearest(E.hdr, E.w, E.h, u, v));
-  float pdf = tex_nearest(E.cache, E.w, E.h, u, v).z;
+  const float4 t = tex_nearest(E.hdr, E.w, E.h, u, v);
+  color = xyz(t);
+  float pdf = t.w;
   float theta = PI * v;
   float sin_theta = max_(sin_(theta), 1e-10f);
   float p_convert = (float)(E.res * E.res / 2) / (TWO_PI * PI * sin_theta);

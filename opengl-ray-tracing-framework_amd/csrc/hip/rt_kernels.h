@@ -50,7 +50,7 @@ struct KParams {
   const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, leaf rank bits} {n3, 0}
   const float4* __restrict__ mats;  // 8 per material
   const float4* __restrict__ hdr;
-  const float4* __restrict__ cache;
+  const float2* __restrict__ cache;  // hdrCache.rg (hdr.w holds hdrCache.b)
   int hdr_w, hdr_h, hdr_res;
   float4* __restrict__ accum;
   unsigned int* __restrict__ counter;

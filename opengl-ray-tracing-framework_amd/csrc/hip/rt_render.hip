@@ -42,7 +42,7 @@ struct rt_ctx {
   std::vector<float> mat_table;  // host copy, 32 floats per material
   // env
   float4* d_hdr = nullptr;
-  float4* d_cache = nullptr;
+  float2* d_cache = nullptr;                  // hdrCache.rg; d_hdr = {hdrMap.rgb, hdrCache.b}
   int hdr_w = 0, hdr_h = 0, hdr_res = 0;
   bool env_set = false;
   // frame
@@ -825,14 +825,16 @@ int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_materi
 int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32_t h, int32_t res) {
   if (!c || !hdr || !cache || w <= 0 || h <= 0) return RT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<float4> a((size_t)w * h), b((size_t)w * h);
+  // {hdrMap.rgb, hdrCache.b} per texel (a direction's colour and pdf in one fetch) + hdrCache.rg
+  std::vector<float4> a((size_t)w * h);
+  std::vector<float2> b((size_t)w * h);
   for (size_t i = 0; i < a.size(); i++) {
-    a[i] = make_float4(hdr[3 * i], hdr[3 * i + 1], hdr[3 * i + 2], 0.0f);
-    b[i] = make_float4(cache[3 * i], cache[3 * i + 1], cache[3 * i + 2], 0.0f);
+    a[i] = make_float4(hdr[3 * i], hdr[3 * i + 1], hdr[3 * i + 2], cache[3 * i + 2]);
+    b[i] = make_float2(cache[3 * i], cache[3 * i + 1]);
   }
   int rc;
   if ((rc = upload(c, (void**)&c->d_hdr, a.data(), a.size() * sizeof(float4)))) return rc;
-  if ((rc = upload(c, (void**)&c->d_cache, b.data(), b.size() * sizeof(float4)))) return rc;
+  if ((rc = upload(c, (void**)&c->d_cache, b.data(), b.size() * sizeof(float2)))) return rc;
   c->hdr_w = w; c->hdr_h = h; c->hdr_res = res;
   c->env_set = true;
   return RT_OK;
