@@ -1,4 +1,4 @@
-# HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE passes) + durations, one frame group of 160 frames
+# HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 note) + kernel durations, one frame group of 160 frames: bash tools/hbm_per_kernel.sh
 export TMPDIR=/tmp
 O=gpurun_out/hbm27; mkdir -p $O
 Q="python3 tools/quick_perf.py --frames 160 --per-launch 160 --count-frames 1"
