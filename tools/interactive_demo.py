@@ -61,4 +61,5 @@ for name, make in phases:
         Path(a.out).mkdir(parents=True, exist_ok=True)
         sl.write_png(str(Path(a.out) / f"{a.config}_{name}.png"), out["image"])
 if a.out:
+    Path(a.out).mkdir(parents=True, exist_ok=True)
     (Path(a.out) / f"{a.config}_interactive.json").write_text(json.dumps(report, indent=1))
