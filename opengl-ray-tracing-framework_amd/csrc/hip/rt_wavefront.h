@@ -768,6 +768,9 @@ constexpr int SH_KEYS = 8;  // 0: no continuation hit; 1 + material id % 7: cont
 #define RT_SH_SORT_MIN (1u << 26)
 #endif
 constexpr unsigned int SH_SORT_MIN = RT_SH_SORT_MIN;  // active paths from which wf_shade sorts
+#ifndef RT_SH_SORT_REL
+#define RT_SH_SORT_REL 1  // N = 8 rank share +0.6%, N = 1 +0.1% over the absolute 64 Mi threshold
+#endif
 
 // what a path's shade iteration will run: the cheap end-of-path / env branch or a bounce on
 // the hit material
@@ -824,7 +827,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   if (threadIdx.x < SH_KEYS) lhist[threadIdx.x] = 0u;
   if (threadIdx.x == 0) lc[0] = lc[1] = 0u;
   __syncthreads();
-  if (W.pass == 0 || na < SH_SORT_MIN) {  // camera pass: hit/miss divergence is low already
+#if RT_SH_SORT_REL
+  // sort only passes holding at least a quarter of the group's path slots (in practice pass 1,
+  // whatever the per-rank pixel share)
+  const bool sort_pass = W.pass != 0 && na >= max(1u << 22, (unsigned)W.n_frames * P.n_work / 4u);
+#else
+  const bool sort_pass = W.pass != 0 && na >= SH_SORT_MIN;
+#endif
+  if (!sort_pass) {  // camera pass: hit/miss divergence is low already
 #pragma unroll
     for (int sub = 0; sub < SH_SUB; sub++) {
       const unsigned int j = (unsigned)sub * 256u + threadIdx.x;
