@@ -6,7 +6,7 @@ HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs
 One *step* = ``--frames-per-step`` (default 1024 = the C3 config's spp)
 progressive frames (1 spp each) of the whole frame, rendered by one rt_render call per rank
 over that rank's pixel tiles with as many frames in flight as HBM holds (rt_set_max_paths:
-216 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 229 GB of path
+208 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 229 GB of path
 state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 57 GB per rank), so
 every rank keeps plenty of work in flight: strong scaling of a fixed frame budget without a
 per-rank latency-floor penalty (tools/rank_sim.py), followed by the
@@ -131,7 +131,7 @@ def main() -> int:
     r.resize(W, H, tile=args.tile, rank=rank, world=world)
     info = r.device_info()
     ad = r.accum_device()
-    # path-state budget: a whole step's frames in flight at once (216 B per pixel-frame: 57 GB
+    # path-state budget: a whole step's frames in flight at once (208 B per pixel-frame: 57 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
     # until the state fits (512 = 229 GB of HBM3E on one GPU)
     path_slots = F * ad["local_tiles"] * args.tile * args.tile

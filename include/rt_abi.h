@@ -49,7 +49,7 @@ enum {
   RT_ERR_LIMIT = -6     /* scene exceeds a kernel limit (leaf > 16 tris, depth > 64) */
 };
 
-/* Frames per kernel batch; the path-state budget (216 B per pixel-frame, RT_MAX_SLOTS, default
+/* Frames per kernel batch; the path-state budget (208 B per pixel-frame, RT_MAX_SLOTS, default
  * 320Mi slots = 69 GB) bounds it too: 161 frames at 1920x1080 on one GPU, all 512 of a bench
  * step on each of 8 tile-sharded GPUs. */
 enum { RT_MAX_FRAMES_PER_LAUNCH = 1024 };
@@ -132,7 +132,7 @@ int rt_set_loop_num(rt_ctx* ctx, int32_t loop_num);
 int rt_get_loop_num(const rt_ctx* ctx, int32_t* loop_num);
 /* Clear this rank's accumulation to zero (fresh FBO contents). */
 int rt_clear_accum(rt_ctx* ctx);
-/* Path-state budget in pixel-frames (216 B each): frames in flight per launch = slots / pixels of
+/* Path-state budget in pixel-frames (208 B each): frames in flight per launch = slots / pixels of
  * this rank, at most RT_MAX_FRAMES_PER_LAUNCH.  0 = RT_MAX_SLOTS from the environment or the
  * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL
  * counterpart: the fragment shader has one path per pixel in flight. */

@@ -27,7 +27,10 @@
 
 namespace rtd {
 
-// per-path flags
+#ifndef RT_S5_PACK  // per-path seed/bounce/flags in 8 B instead of 16 (frame from the slot)
+#define RT_S5_PACK 1
+#endif
+// per-path flags (< 256: packed with the bounce when RT_S5_PACK)
 enum : uint32_t {
   PF_SHADOW = 1u,      // a shadow ray was traced for the current bounce (c_nee pending)
   PF_CMED = 2u,        // medium-emissive term pending (RT:1438)
@@ -42,7 +45,11 @@ struct WFState {
   float4* __restrict__ s2;   // evf.xyz, Le0.y
   float4* __restrict__ s3;   // cnee.xyz, Le0.z
   float4* __restrict__ s4;   // cmed.xyz, -
-  uint4* __restrict__ s5;    // wseed, bounce, flags, -
+#if RT_S5_PACK
+  uint2* __restrict__ s5;    // wseed, bounce << 8 | flags (the frame is slot % frames: pixel-major)
+#else
+  uint4* __restrict__ s5;    // wseed, bounce, flags, frame
+#endif
   float4* __restrict__ ro;   // continuation ray origin (xyz)
   float4* __restrict__ rd;   // continuation ray direction
   float4* __restrict__ so;   // shadow ray origin
@@ -197,7 +204,12 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
       const f3 d = camera_ray(P, S, slot, wseed, f);
       S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
       S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+#if RT_S5_PACK
+      S.s5[slot] = make_uint2(wseed, PF_CONT | PF_CAMERA);
+      (void)f;
+#else
       S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
+#endif
       S.queue[in][qbase + j] = (int)(slot << 1);
       S.active[in][abase + j] = (int)slot;
     }
@@ -775,7 +787,11 @@ constexpr unsigned int SH_SORT_MIN = RT_SH_SORT_MIN;  // active paths from which
 // what a path's shade iteration will run: the cheap end-of-path / env branch or a bounce on
 // the hit material
 RTD int shade_key(const KParams& P, const WFState& S, int path) {
+#if RT_S5_PACK
+  const uint32_t flags = S.s5[path].y & 0xffu;
+#else
   const uint32_t flags = S.s5[path].z;
+#endif
   const int t = S.res[2 * path].x;
   if (!(flags & PF_CONT) || t < 0) return 0;
 #if RT_SH_KEY_MAT
@@ -887,7 +903,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
         a5 = make_uint4(cseed, 0u, PF_CONT | PF_CAMERA, cframe);
         cam_d = make_float4(d.x, d.y, d.z, 0.0f);
       } else {
+#if RT_S5_PACK
+        const uint2 p5 = S.s5[path];
+        const unsigned int nfr = (unsigned int)W.n_frames;
+        a5 = make_uint4(p5.x, p5.y >> 8, p5.y & 0xffu, (unsigned int)path % nfr);
+#else
         a5 = S.s5[path];
+#endif
       }
       // every load of the path's state issues at once: camera paths exist only in pass 0 (a
       // uniform test), so no load waits for the flags; the flags still decide what is used
@@ -1169,7 +1191,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
       if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
       if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
+#if RT_S5_PACK
+      S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
+#else
       S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
+#endif
       if (qCont) {
         S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
         S.rd[path] = make_float4(contD.x, contD.y, contD.z, 0.0f);
