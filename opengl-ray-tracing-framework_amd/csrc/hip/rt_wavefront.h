@@ -491,8 +491,9 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #define RT_TRACE_WPE 1
 #endif
 #ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s;
-                       // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%
-#define RT_REFILL_MIN 24
+                       // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%;
+                       // final build: 20 / 24 / 28 -> +0.3% / 0 / -0.9%
+#define RT_REFILL_MIN 20
 #endif
 #ifndef RT_TAIL_CHUNK  // rays per claim near the end of a pass queue (and per participating wave)
 #define RT_TAIL_CHUNK 64u
@@ -769,8 +770,9 @@ void wf_trace(const WFParams W) {
 // ----------------------------------------------------------------------------- shade
 // Paths per block-iteration of wf_shade = 256 x SH_SUB: the block stages its queue / active
 // entries in LDS and claims global space with one atomic per list per block-iteration.
-#ifndef RT_SH_SUB  // C3 on the rebuilt tree: 1 / 2 / 4 / 8 -> -1.2% / 0 / -0.9% / -1.4% (tools/ab_proc.py)
-#define RT_SH_SUB 2
+#ifndef RT_SH_SUB  // C3 on the rebuilt tree: 1 / 2 / 4 / 8 -> -1.2% / 0 / -0.9% / -1.4% (tools/ab_proc.py);
+                   // final build: 3 vs 2 +0.4%
+#define RT_SH_SUB 3
 #endif
 #ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0: +1.0%)
 #define RT_SH_KEY_MAT 0
