@@ -7,24 +7,28 @@ One *step* = ``--frames-per-step`` (default 1024 = the C3 config's spp, SURVEY ย
 progressive frames (1 spp each) of the whole frame, rendered by one rt_render call per rank
 over that rank's pixel tiles with as many frames in flight as HBM holds (rt_set_max_paths:
 208 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 229 GB of path
-state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 57 GB per rank), so
-every rank keeps plenty of work in flight: strong scaling of a fixed frame budget without a
-per-rank latency-floor penalty (tools/rank_sim.py), followed by the
-frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over xGMI via
-torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
+state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 57 GB per rank),
+followed by the frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over
+xGMI via torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
 
     python bench.py [--gpus 1] [--steps 10] [--warmup 2]
+    python bench.py --gpus N ...          (spawns N rank processes itself, one per GPU)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+    python bench.py --dry-run --gpus 2    (CPU: launcher, frame plan and gloo gather only)
 
 Rank 0 prints ONE JSON line.  value = rays traced by all ranks / max-over-ranks wall time
 of the timed steps (barrier + synchronize on both sides).  Rays are counted on the device
 (camera + NEE shadow + continuation = every hitBVH call of the reference, RT:1386/1480/1528).
+randOrigin_k for any number of frames comes from the in-tree restatement of glibc rand()
+(main.cpp:190, rtamd/configs.py rand_origins).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,15 +39,26 @@ sys.path.insert(0, str(ROOT / "opengl-ray-tracing-framework_amd"))
 import numpy as np  # noqa: E402
 
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+L2_PEAK_GBS = 34500.0     # aggregate L2 bandwidth, measured (MI355X_MICROARCH.md ยงL2)
+N_SIMD = 256 * 4          # CUs x SIMDs
+VALU_CYC = 2              # cycles per wave64 VALU instruction on a SIMD-32 (157.3 TF fp32 = 1024 x 64 x 2.4 GHz)
 # SURVEY.md ยง8(d): algorithmic bytes per traversal from the reference's visit counts
 #   64 B per internal pop (16 B node ints + two 24-B child AABBs), 16 B per leaf pop,
 #   36 B per triangle test (positions), 132 B per closer-hit update (normals + material),
 #   12 B per HDR texel fetch, 12 B per cache texel fetch, + 24 B per pixel-frame (accum r/w)
 B_INT, B_LEAF, B_TRI, B_UPD, B_ENV, B_CACHE, B_PIXEL = 64, 16, 36, 132, 12, 12, 24
+# wf_trace's own HBM stream per ray (the ~25 MB scene stays in L2 / Infinity Cache): a
+# secondary ray reads its 4-B queue entry and its 32-B origin/direction and writes its 8-B
+# result; a camera ray is rebuilt from the per-pixel camera table (16 B per pixel, shared by
+# the pixel's frames) and writes its 8-B result
+B_RAY_SECONDARY, B_RAY_CAMERA = 4 + 32 + 8, 8
+# wf_trace's own traversal bytes per visit (served from L2 / MALL): a 128-B 4-wide node, a
+# 48-B triangle record
+B_QNODE, B_TRI_REC = 128, 48
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -56,10 +71,49 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample: oracle frames until this wall time (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--single-frames", type=int, default=64,
+                    help="frames rendered one per rt_render call after the timed region (ms_per_frame_single)")
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: launcher, frame plan, tiling and the gloo gather only (CPU tests)")
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a torch.distributed launcher: start N rank processes (one per
+    GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, wait for all, and forward rank 0's
+    JSON line.  This parent never touches the GPU (no torch import), so nothing is initialised
+    in it before the children start."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out0 = procs[0].communicate()[0] if procs else ""
+    rcs = [p.wait() for p in procs]
+    line = next((ln for ln in reversed(out0.splitlines()) if ln.startswith("{")), None)
+    if any(rcs) or line is None:
+        print(f"bench.py: rank exit codes {rcs}" + ("" if line else "; rank 0 printed no JSON line"),
+              file=sys.stderr)
+        return next((rc for rc in rcs if rc), 1)
+    print(line, flush=True)
+    return 0
+
+
+# ------------------------------------------------------------------------------ CPU baseline
 def cpu_baseline(sd, env, W, H, fp, seconds: float, threads: int):
     """The oracle (CPU restatement of the shader, OpenMP) on whole frames 1..k of the same
     workload until `seconds` of wall time; returns the JSON object and the ยง8(d) counters."""
@@ -93,24 +147,132 @@ def cpu_baseline(sd, env, W, H, fp, seconds: float, threads: int):
     return obj, tot
 
 
-def main() -> int:
-    args = parse_args()
+# ------------------------------------------------------------------------------ roofline
+def load_profile(config: str, W: int, H: int, F: int, slots: int):
+    """profiles/pmc_<config>.json (tools/profile_gpu.sh + tools/summarize_profile.py): rocprofv3
+    kernel-trace duration and PMC counters of the bench workload's wf_trace launches; used only
+    when its workload key matches this run."""
+    p = ROOT / "profiles" / f"pmc_{config}.json"
+    if not p.exists():
+        return None
+    d = json.loads(p.read_text())
+    if (d.get("kernel") == "wf_trace" and d.get("width") == W and d.get("height") == H
+            and d.get("frames_per_step") == F and d.get("path_slots_per_rank") == slots):
+        d["_file"] = str(p.relative_to(ROOT))
+        return d
+    return None
+
+
+def roofline(st, vis, cnt, prof, trace_ms):
+    """wf_trace (the dominant kernel) against the HBM roofline, with its algorithmic HBM bytes:
+    the path-state stream it must move (per ray, B_RAY_*; the scene is cache-resident).
+    traffic = rocprofv3 PMC HBM bytes per launch.  Also: the same kernel's VALU issue rate (its
+    actual limiter), its own traversal bytes against the L2 bandwidth that serves them, and the
+    reference-equivalent ยง8(d) figure (reference visit counts), labelled as such, never as frac."""
+    launches = max(1, st["trace_launches"])
+    rays_l = st["rays"] / launches
+    cam_l = st["samples"] / launches                      # one camera ray per sample
+    alg = (B_RAY_SECONDARY * (rays_l - cam_l) + B_RAY_CAMERA * cam_l)
+    sec = trace_ms * 1e-3
+    out = {"bound": "hbm", "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "rays_per_launch": round(rays_l),
+           "algorithmic_bytes_per_launch": round(alg),
+           "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "camera": B_RAY_CAMERA}}
+    if prof:
+        out["traffic"] = prof.get("hbm_bytes_per_launch")
+        out["profile"] = prof["_file"]
+        out["profile_avg_launch_ms"] = prof.get("avg_launch_ms")
+        sq = prof.get("SQ", {})
+        pl = prof.get("avg_launch_ms") or trace_ms
+        clk = prof.get("clock_ghz") or 2.4
+        if sq.get("SQ_INSTS_VALU"):
+            v = {"insts_per_launch": round(sq["SQ_INSTS_VALU"]), "cycles_per_inst": VALU_CYC, "clock_ghz": clk,
+                 "issue_frac": round(sq["SQ_INSTS_VALU"] * VALU_CYC / (N_SIMD * clk * 1e9 * pl * 1e-3), 4),
+                 "insts_per_ray": round(sq["SQ_INSTS_VALU"] / rays_l, 1)}
+            if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("SQ_THREAD_CYCLES_VALU"):
+                v["lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64 * sq["SQ_ACTIVE_INST_VALU"]), 4)
+            out["valu"] = v
+    if vis and vis.get("rays"):
+        own = (B_QNODE * vis["internal_pops"] + B_TRI_REC * vis["tri_tests"]) / vis["rays"]
+        out["l2"] = {"own_traversal_bytes_per_ray": round(own, 1),
+                     "achieved": round(own * rays_l / sec / 1e9, 1), "peak": L2_PEAK_GBS,
+                     "frac": round(own * rays_l / sec / 1e9 / L2_PEAK_GBS, 4)}
+    if cnt:
+        per_ray = (B_INT * cnt["internal_pops"] + B_LEAF * cnt["leaf_pops"] + B_TRI * cnt["tri_tests"] +
+                   B_UPD * cnt["closer_updates"]) / cnt["rays"]
+        out["reference_equivalent"] = {
+            "bytes_per_ray": round(per_ray, 1), "gbs": round(per_ray * rays_l / sec / 1e9, 1),
+            "note": "SURVEY ยง8(d) bytes of the reference's own exhaustive traversal (oracle visit counts) per "
+                    "ray traced here; the device traversal visits fewer nodes, so this is not a bandwidth"}
+    return out
+
+
+# ------------------------------------------------------------------------------ dry run
+def dry_run(args, rank: int, world: int) -> int:
+    """CPU rehearsal of the multi-rank bench: frame plan (randOrigin for every frame), each
+    rank's tile share, and the frame-end gather over gloo with max-over-ranks timing."""
+    import torch
+    import torch.distributed as dist
+
+    from rtamd import configs as cf
+    from rtamd import tiling
+
+    cfg = cf.CONFIGS[args.config]
+    W, H = args.width or cfg.width, args.height or cfg.height
+    F, steps, warm = args.frames_per_step, args.steps, args.warmup
+    total_frames = (warm + steps) * F + 1 + args.single_frames
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    ro = cf.rand_origins(total_frames)
+    mine = tiling.local_tiles(W, H, args.tile, args.tile, rank, world)
+    mlt = tiling.max_local_tiles(W, H, args.tile, args.tile, world)
+    px = sum(tiling.tile_rect(t, W, H, args.tile, args.tile)[2] * tiling.tile_rect(t, W, H, args.tile, args.tile)[3]
+             for t in mine)
+    t0 = time.perf_counter()
+    local = torch.full((mlt, 4), float(rank))
+    if world > 1:
+        parts = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
+        dist.gather(local, gather_list=parts, dst=0)
+        pxs = torch.tensor([float(px)])
+        dist.all_reduce(pxs)
+        elapsed = torch.tensor([time.perf_counter() - t0])
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        total_px = int(pxs[0])
+        ok = rank != 0 or all(int(p[0, 0]) == r for r, p in enumerate(parts))
+    else:
+        total_px, ok, elapsed = px, True, torch.tensor([time.perf_counter() - t0])
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": steps,
+                          "warmup": warm, "dry_run": True, "frames_planned": total_frames,
+                          "rand_origin_last": float(ro[-1]), "pixels_covered": total_px,
+                          "frame_pixels": W * H, "gather_ok": bool(ok),
+                          "gather_ms": round(float(elapsed[0]) * 1e3, 3)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if (total_px == W * H and ok) else 1
+
+
+# ------------------------------------------------------------------------------ bench
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus N>1 must be launched with torch.distributed.run (one process per GPU)",
-                  file=sys.stderr)
-            return 2
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args, rank, world)
     import torch
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    else:
-        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
 
     from rtamd import configs as cf
     from rtamd.renderer import RT_FLAG_COUNT_VISITS, Renderer
@@ -118,18 +280,23 @@ def main() -> int:
     cfg = cf.CONFIGS[args.config]
     W, H = args.width or cfg.width, args.height or cfg.height
     F, steps, warm = args.frames_per_step, args.steps, args.warmup
-    total_frames = (warm + steps) * F + 1
+    n_single = max(0, args.single_frames)
+    total_frames = (warm + steps) * F + 1 + n_single
     sd = cf.config_scene(args.config)
     env = cf.load_env()
     fp = cf.frame_params(W, H)
+    ro = cf.rand_origins(total_frames)
 
+    # One stream for everything: the renderer's kernels and copies and torch's RCCL collectives
+    # (ProcessGroupNCCL orders its internal stream after the *current* stream), so the gather reads
+    # finished tiles and the assemble reads the gathered ones.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     r = Renderer(local_rank)
-    stream = torch.cuda.current_stream()
-    r.set_stream(stream.cuda_stream)  # kernels, copies and RCCL collectives on one stream
+    r.set_stream(stream.cuda_stream)
     r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(*env)
     r.resize(W, H, tile=args.tile, rank=rank, world=world)
-    info = r.device_info()
     ad = r.accum_device()
     # path-state budget: a whole step's frames in flight at once (208 B per pixel-frame: 57 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
@@ -140,7 +307,6 @@ def main() -> int:
     local = torch.empty(nfloat, dtype=torch.float32, device="cuda")
     gathered = torch.empty(world * nfloat, dtype=torch.float32, device="cuda") if rank == 0 else None
     frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
-    ro = cf.rand_origins(total_frames)
 
     def step(k: int) -> None:
         r.render_async(fp, ro[k * F:(k + 1) * F])
@@ -155,9 +321,12 @@ def main() -> int:
         if rank == 0:
             r.assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
 
+    t_w = time.perf_counter()
     for k in range(warm):
         step(k)
     torch.cuda.synchronize()
+    if rank == 0:
+        print(f"bench: warmup {warm} x {F} frames in {time.perf_counter() - t_w:.1f} s", file=sys.stderr, flush=True)
     r.reset_stats()
     if dist:
         dist.barrier()
@@ -182,6 +351,26 @@ def main() -> int:
     else:
         rays, samples = float(st["rays"]), float(st["samples"])
 
+    # the reference's usage pattern (main.cpp:165-200): one frame per draw, outside the timed
+    # region; throughput of back-to-back single-frame calls and the latency of a synchronised one
+    base = (warm + steps) * F
+    single = {}
+    if n_single > 0:
+        r.render_async(fp, ro[base:base + 1])
+        r.synchronize()
+        t1 = time.perf_counter()
+        for k in range(n_single):
+            r.render_async(fp, ro[base + k:base + k + 1])
+        r.synchronize()
+        single["ms_per_frame_single"] = round((time.perf_counter() - t1) * 1e3 / n_single, 3)
+        lat = []
+        for k in range(min(16, n_single)):
+            t2 = time.perf_counter()
+            r.render_async(fp, ro[base + k:base + k + 1])
+            r.synchronize()
+            lat.append(time.perf_counter() - t2)
+        single["ms_single_frame_latency"] = round(float(np.median(lat)) * 1e3, 3)
+
     # own-traversal visit counts (one extra frame, outside the timed region)
     r.reset_stats()
     r.render(cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS), ro[-1:])
@@ -203,7 +392,8 @@ def main() -> int:
         "steps": steps,
         "warmup": warm,
         "ms_per_step": round(elapsed * 1e3 / steps, 3),
-        "ms_per_frame": round(elapsed * 1e3 / (steps * F), 3),
+        "ms_per_frame": round(elapsed * 1e3 / (steps * F), 4),
+        **single,
         "msamples_per_s": round(samples / elapsed / 1e6, 2),
         "rays_per_sample": round(rays / max(1.0, samples), 4),
         "higher_is_better": True,
@@ -211,10 +401,11 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "f32",
         "data": "reference scene assets (loong_100000.obj, floor.obj, peppermint_powerplant_1k.hdr); "
-                "randOrigin from glibc srand(20221002)",
+                "randOrigin from glibc srand(20221002) (in-tree restatement of rand())",
         "config": {"workload": f"{cfg.name}: {cfg.note}; {W}x{H}, maxBounce 8, BSDF+MIS+env",
                    "width": W, "height": H, "frames_per_step": F, "spp_timed": steps * F,
-                   "tile": args.tile, "path_slots_per_rank": path_slots, "parallelism": f"pixel-tiles x{world} + frame-end gather",
+                   "tile": args.tile, "path_slots_per_rank": path_slots,
+                   "parallelism": f"pixel-tiles x{world} + frame-end gather",
                    "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
         "kernel": {"name": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "launches": st["trace_launches"],
                    "render_call_ms": round(launch_ms, 4), "render_calls": st["launches"],
@@ -226,48 +417,12 @@ def main() -> int:
                                         "leaf": round(vis["leaf_pops"] / vis["rays"], 2),
                                         "tri": round(vis["tri_tests"] / vis["rays"], 2)}
 
-    # CPU baseline (rank 0, N = 1 only) and the ยง8(d) per-ray byte figure from its counters
+    # CPU baseline (rank 0, N = 1 only) and the ยง8(d) per-ray figure from its counters
     cnt = None
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"], cnt = cpu_baseline(sd, env, W, H, fp, args.cpu_seconds, args.cpu_threads)
-    pmc = ROOT / "profiles" / f"pmc_traffic_{args.config}.json"
-    traffic = None
-    if pmc.exists():
-        p = json.loads(pmc.read_text())
-        if (p.get("kernel") == "wf_trace" and p.get("width") == W and p.get("height") == H
-                and p.get("frames_per_launch") == F and p.get("path_slots_per_rank") == path_slots):
-            traffic = p.get("hbm_bytes_per_launch")
-    if cnt is not None:
-        # dominant kernel = wf_trace: the reference traversal's bytes per ray (SURVEY ยง8(d) terms of
-        # hitBVH: internal / leaf / triangle / closer-hit) x rays per trace launch / avg launch time
-        per_ray = (B_INT * cnt["internal_pops"] + B_LEAF * cnt["leaf_pops"] + B_TRI * cnt["tri_tests"] +
-                   B_UPD * cnt["closer_updates"]) / cnt["rays"]
-        rays_per_launch = st["rays"] / max(1, st["trace_launches"])
-        bytes_per_launch = per_ray * rays_per_launch
-        achieved = bytes_per_launch / (trace_ms * 1e-3) / 1e9
-        # whole path (every kernel of a render call, all ยง8(d) terms incl. env/cache/accumulation)
-        per_sample = (per_ray * cnt["rays"] + B_ENV * cnt["env_fetches"] + B_CACHE * cnt["cache_fetches"]) \
-            / cnt["samples"] + B_PIXEL
-        path_gbs = per_sample * st["samples"] / (st["kernel_ms"] * 1e-3) / 1e9
-        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                           "kernel": "wf_trace", "algorithmic_bytes_per_ray": round(per_ray, 1),
-                           "rays_per_launch": round(rays_per_launch), "bytes_per_launch": round(bytes_per_launch),
-                           "path_algorithmic_bytes_per_sample": round(per_sample, 1),
-                           "path_achieved_gbs": round(path_gbs, 1),
-                           "note": "algorithmic bytes from the reference traversal's visit counts (SURVEY ยง8(d)); "
-                                   "frac can exceed 1 because the device traversal does ~2.4x fewer node visits "
-                                   "(closest-hit culling + 4-wide nodes) and reads the ~25 MB scene from L2/MALL: "
-                                   "traffic (PMC) is the real HBM bytes per launch; the kernel is VALU-issue / "
-                                   "latency bound, not HBM bound"}
-        if vis["rays"]:
-            # the same per-ray figure over the device traversal's own visits (128-B 4-wide nodes,
-            # 48-B triangle records, leaves cost nothing: their range lives in the parent)
-            own = (128 * vis["internal_pops"] + 48 * vis["tri_tests"]) / vis["rays"]
-            out["roofline"]["own_traversal_bytes_per_ray"] = round(own, 1)
-    else:
-        out["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                           "traffic": traffic, "note": "per-ray bytes need the rank-0 N=1 oracle sample"}
+    prof = load_profile(args.config, W, H, F, path_slots)
+    out["roofline"] = roofline(st, vis, cnt, prof, trace_ms)
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

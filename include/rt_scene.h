@@ -113,8 +113,13 @@ void rts_free(void* p);
 /* ---- camera / frame parameters ------------------------------------------------ */
 /* out[17] = front[3], right[3], up[3], left_bottom_corner[3], half_h, half_w, (3 reserved) */
 int rts_camera(float yaw_deg, float pitch_deg, float zoom_deg, float screen_ratio, float* out);
-/* randOrigin_k = 674764 * (rand()/(RAND_MAX+1.0) + 1) after srand(seed), glibc rand. */
+/* randOrigin_k = 674764 * (rand()/(RAND_MAX+1.0) + 1) after srand(seed) (main.cpp:190,
+ * src/core/Utility.h:11-17), any n: glibc's rand() is restated in-tree (rts_glibc_rand), so the
+ * list does not depend on the host libc. */
 int rts_cpu_rand_origins(unsigned int seed, int n, float* out);
+/* The first n values of glibc rand() after srand(seed) (stdlib/random_r.c TYPE_3 generator,
+ * restated; identical to the libc's on glibc systems). */
+int rts_glibc_rand(unsigned int seed, int n, int* out);
 
 /* 8-bit RGB PNG (stbi_write_png in SaveFrame, src/core/Utility.h:19-30): width*height*3 bytes,
  * row 0 = top (rt_tonemap's output order).  Stored (uncompressed) deflate, no zlib needed. */

@@ -522,6 +522,25 @@ hipEvent_t take_event(rt_ctx* c) {
   return e;
 }
 
+// Timing events of launches not yet folded into kernel_ms / trace_ms: a front end that never
+// calls rt_synchronize (it waits on its own stream or events) would otherwise grow these lists
+// without bound.  Past `cap` pending pairs, the oldest are waited for, folded and recycled.
+int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap) {
+  if (ev.size() <= cap) return RT_OK;
+  const size_t n = ev.size() - cap / 2;
+  HIPCHK(c, hipEventSynchronize(ev[n - 1].second));
+  for (size_t i = 0; i < n; i++) {
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, ev[i].first, ev[i].second));
+    acc_ms += ms;
+    c->event_pool.push_back(ev[i].first);
+    c->event_pool.push_back(ev[i].second);
+  }
+  ev.erase(ev.begin(), ev.begin() + (ptrdiff_t)n);
+  return RT_OK;
+}
+constexpr size_t kMaxPendingEvents = 4096;
+
 // Frames in flight per launch = path-state budget / pixels of this rank.  The state grows on
 // demand in rt_render_async, so interactive 1-frame use stays small.  More frames per launch
 // amortise the per-pass latency floor of the few longest rays (C3 1080p: 16 frames 1.07, 64
@@ -846,7 +865,11 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   if (tl.tile_w <= 0 || tl.tile_h <= 0 || (tl.tile_w % 8) || (tl.tile_h % 8) || tl.world <= 0 || tl.rank < 0 ||
       tl.rank >= tl.world)
     return fail(c, RT_ERR_ARG, "bad tiling (tile sizes must be positive multiples of 8, 0 <= rank < world)");
+  if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
   HIPCHK(c, hipSetDevice(c->device));
+  // the old pixel lists / accumulation no longer describe the frame from here on: a failure
+  // below leaves the context un-sized (rt_render_async then refuses) rather than half-resized
+  c->frame_set = false;
   c->W = width; c->H = height;
   c->tile_w = tl.tile_w; c->tile_h = tl.tile_h; c->rank = tl.rank; c->world = tl.world;
   c->tiles_x = (width + tl.tile_w - 1) / tl.tile_w;
@@ -873,7 +896,6 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
       acc.push_back((unsigned)(lt * tpx + ly * tl.tile_w + lx));
     }
   }
-  if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
   c->n_valid = (int)xy.size();
   dfree(c->d_pix);
   dfree(c->d_cam);
@@ -1182,6 +1204,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->events.push_back({e0, e1});
     c->launches++;
+    int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents);
+    if (!frc) frc = fold_events(c, c->events, c->kernel_ms, kMaxPendingEvents);
+    if (frc) return frc;
   }
   return RT_OK;
 }

@@ -1246,12 +1246,46 @@ int rts_write_png(const char* path, int width, int height, const uint8_t* rgb) {
   return ok ? RTS_OK : RTS_ERR_IO;
 }
 
+// glibc rand() restated (stdlib/random_r.c, TYPE_3: x^31 + x^3 + 1 additive feedback over 31
+// words, the default state of srand/rand), so the randOrigin list does not depend on the libc
+// of the machine it runs on and has no length limit:
+//   r[0] = seed (0 -> 1); r[i] = 16807 * r[i-1] mod (2^31 - 1), i = 1..30 (Schrage's form, as
+//   glibc's __srandom_r); then r[i] = r[i-31] + r[i-3] (mod 2^32) for i >= 31, the first 310
+//   outputs discarded (10 * 31), and rand() = r[i] >> 1 (RAND_MAX = 2^31 - 1).
+int rts_glibc_rand(unsigned int seed, int n, int* out) {
+  if (!out || n < 0) return RTS_ERR_ARG;
+  uint32_t r[34];
+  int32_t word = seed == 0 ? 1 : (int32_t)seed;
+  r[0] = (uint32_t)word;
+  for (int i = 1; i < 31; i++) {
+    const int32_t hi = word / 127773, lo = word % 127773;
+    word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    r[i] = (uint32_t)word;
+  }
+  // ring of the last 31 words: front = i - 31, rear = i - 3
+  uint32_t ring[31];
+  for (int i = 0; i < 31; i++) ring[i] = r[i];
+  int f = 3, b = 0;  // glibc: fptr = state + SEP_3 (3), rptr = state
+  auto next = [&]() -> uint32_t {
+    ring[f] += ring[b];
+    const uint32_t v = ring[f];
+    if (++f == 31) f = 0;
+    if (++b == 31) b = 0;
+    return v >> 1;
+  };
+  for (int i = 0; i < 310; i++) (void)next();
+  for (int k = 0; k < n; k++) out[k] = (int)next();
+  return RTS_OK;
+}
+
 int rts_cpu_rand_origins(unsigned int seed, int n, float* out) {
   if (!out || n < 0) return RTS_ERR_ARG;
-  srand(seed);
+  std::vector<int> r((size_t)n);
+  if (n > 0) rts_glibc_rand(seed, n, r.data());
   for (int k = 0; k < n; k++) {
-    float r = (float)((float)rand() / (RAND_MAX + 1.0));  // GetCPURandom, src/core/Utility.h:15-17
-    out[k] = 674764.0f * (r + 1.0f);                      // main.cpp:190
+    float x = (float)((float)r[k] / (2147483647 + 1.0));  // GetCPURandom, src/core/Utility.h:15-17
+    out[k] = 674764.0f * (x + 1.0f);                      // main.cpp:190
   }
   return RTS_OK;
 }

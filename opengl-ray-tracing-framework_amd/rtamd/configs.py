@@ -148,14 +148,25 @@ def frame_params(width: int, height: int, **overrides) -> FrameParams:
     return fp
 
 
+@lru_cache(maxsize=1)
+def _fixture_bits() -> np.ndarray:
+    with open(GOLDEN_DIR / "rand_origins.json") as f:
+        return np.array(json.load(f)["bits"], dtype=np.uint32)
+
+
 def rand_origins(n: int, offset: int = 0) -> np.ndarray:
-    """randOrigin for frames offset+1 .. offset+n (committed fixture, glibc srand(20221002))."""
-    path = GOLDEN_DIR / "rand_origins.json"
-    with open(path) as f:
-        bits = np.array(json.load(f)["bits"], dtype=np.uint32)
-    if offset + n > len(bits):
-        raise ValueError(f"only {len(bits)} committed randOrigin values")
-    return bits[offset:offset + n].view(np.float32).copy()
+    """randOrigin for frames offset+1 .. offset+n after glibc srand(20221002) (main.cpp:190), any
+    length: generated by librtscene's in-tree restatement of glibc rand() (rts_glibc_rand), and
+    the part that overlaps the committed 16,384-frame fixture (made with the libc's own rand())
+    must equal it bit for bit."""
+    if n < 0 or offset < 0:
+        raise ValueError("rand_origins: n and offset must be >= 0")
+    out = sl.cpu_rand_origins(RAND_SEED, offset + n)[offset:]
+    bits = _fixture_bits()
+    k = max(0, min(len(bits), offset + n) - offset)
+    if k and not np.array_equal(out[:k].view(np.uint32), bits[offset:offset + k]):
+        raise RuntimeError("randOrigin generator disagrees with tests/golden/rand_origins.json")
+    return out
 
 
 def oracle_frame_params(fp: FrameParams, loop_num: int, rand_origin: float) -> dict:

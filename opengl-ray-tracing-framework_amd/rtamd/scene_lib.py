@@ -111,6 +111,7 @@ def lib() -> C.CDLL:
         L.rts_free.restype = None
         L.rts_camera.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, _f32p]
         L.rts_cpu_rand_origins.argtypes = [C.c_uint, C.c_int, _f32p]
+        L.rts_glibc_rand.argtypes = [C.c_uint, C.c_int, C.POINTER(C.c_int)]
         L.rts_write_png.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
@@ -301,8 +302,16 @@ def camera(yaw: float, pitch: float, zoom: float, ratio: float) -> dict:
 
 
 def cpu_rand_origins(seed: int, n: int) -> np.ndarray:
+    """randOrigin_1..n after srand(seed) (main.cpp:190; glibc rand restated in librtscene)."""
     out = np.zeros(n, np.float32)
     _check(lib().rts_cpu_rand_origins(seed, n, _fp(out)), "rts_cpu_rand_origins")
+    return out
+
+
+def glibc_rand(seed: int, n: int) -> np.ndarray:
+    """The first n glibc rand() values after srand(seed) (rts_glibc_rand)."""
+    out = np.zeros(n, np.int32)
+    _check(lib().rts_glibc_rand(seed, n, out.ctypes.data_as(C.POINTER(C.c_int))), "rts_glibc_rand")
     return out
 
 

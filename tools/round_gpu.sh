@@ -1,15 +1,16 @@
 #!/bin/bash
 # Round evidence on the GPU box (repo root): GPU tests, rocprofv3 kernel trace + PMC passes of
 # the bench workload, their summary into profiles/ (PMC traffic per wf_trace launch), then the
-# default bench line (which reads that traffic).  profiles/ comes back via gpurun_out/profiles.
+# driver's bench command (which reads that summary).  profiles/ comes back via gpurun_out/profiles.
+set -o pipefail
 export TMPDIR=/tmp
-TAG=${TAG:-r01_C3}
-mkdir -p gpurun_out
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+TAG=${TAG:-r02_C3}
+mkdir -p gpurun_out/profiles
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
 bash tools/profile_gpu.sh gpurun_out/prof || { echo "profile failed"; exit 1; }
 python3 tools/summarize_profile.py gpurun_out/prof $TAG \
-  '{"config": "C3", "width": 1920, "height": 1080, "frames_per_launch": 1024, "path_slots_per_rank": 2139095040, "command": "bash tools/profile_gpu.sh (bench.py --steps 5 --warmup 1 --cpu-seconds 0)"}' > gpurun_out/summary.log || exit 1
-timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
+  '{"config": "C3", "width": 1920, "height": 1080, "frames_per_step": 1024, "path_slots_per_rank": 2139095040, "command": "bash tools/profile_gpu.sh (bench.py --steps 3 --warmup 1 --cpu-seconds 0 --single-frames 0)"}' > gpurun_out/summary.log || exit 1
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
-mkdir -p gpurun_out/profiles && cp profiles/${TAG}_* profiles/pmc_traffic_C3.json gpurun_out/profiles/
+cp profiles/${TAG}_* profiles/pmc_C3.json gpurun_out/profiles/
