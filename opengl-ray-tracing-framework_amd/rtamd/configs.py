@@ -53,7 +53,7 @@ MATERIALS = {
 @dataclasses.dataclass(frozen=True)
 class Obj:
     mesh: str          # asset name
-    material: str
+    material: object   # a MATERIALS key or an sl.Material
     rotate: tuple
     translate: tuple
     scale: tuple
@@ -126,7 +126,8 @@ def build_scene(objects, leaf_size: int = 8) -> SceneData:
     s = sl.Scene()
     ranges = []
     for o in objects:
-        ranges.append(s.add_mesh(load_mesh(o.mesh), MATERIALS[o.material], o.rotate, o.translate, o.scale, o.smooth))
+        mat = o.material if isinstance(o.material, sl.Material) else MATERIALS[o.material]
+        ranges.append(s.add_mesh(load_mesh(o.mesh), mat, o.rotate, o.translate, o.scale, o.smooth))
     s.build_bvh(leaf_size)
     tri, nodes = s.encode()
     return SceneData("custom", s.counts(), tri, nodes, s.export_soa(), s.nodes(), ranges)
