@@ -43,6 +43,7 @@ struct KParams {
   const QNode* __restrict__ qnodes;  // 4-wide collapse of `nodes` (wavefront trace, TW_WIDE)
   int qroot;
   int lds_entries;                  // wavefront traversal: stack entries kept in LDS
+  float cull_eps;                   // culling bound: accepted hit points lie within this of their box
   int pool_chunk;                   // wavefront traversal: rays claimed per queue atomic
   int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]
   unsigned int ovf_lanes;
@@ -76,9 +77,15 @@ RTD float slab(f3 o, f3 inv, f3 AA, f3 BB, float& t0_out) {
   return (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
 }
 
-// Culling bound: a popped subtree whose box entry lies beyond the best hit by more than
-// the triangle-distance rounding can hold no closer hit.
-RTD float cull_limit(float best) { return best + 1e-3f + best * 1e-3f; }
+// Culling bound: a popped subtree whose box entry lies beyond this can hold no hit the reference
+// would accept at dist <= best.  Accepted hit points lie within P.cull_eps of their triangle's
+// boxes (cull_bound_stats in rt_render.hip), so a triangle's t is at least t0 - cull_eps *
+// max|1/d_a|; the 1e-3 terms cover the relative rounding of t0, t and dist = t - 1e-5.  A ray with
+// a zero direction component (1/d infinite) is never culled.
+RTD float cull_limit(float best, float eps, float ix, float iy, float iz) {
+  const float m = fmaxf(fabsf(ix), fmaxf(fabsf(iy), fabsf(iz)));
+  return best + 1e-3f + best * 1e-3f + eps * m;
+}
 
 template <bool COUNT>
 RTD void trace(const KParams& P, f3 o, f3 d, bool anyhit, bool cull, int* __restrict__ sref,
@@ -142,7 +149,7 @@ RTD void trace(const KParams& P, f3 o, f3 d, bool anyhit, bool cull, int* __rest
       } else if (d2 > 0) {
         nearRef = nd.ref.y; nearD = e2; descend = true;
       }
-      if (descend && cull && nearD > cull_limit(best)) descend = false;
+      if (descend && cull && nearD > cull_limit(best, P.cull_eps, inv.x, inv.y, inv.z)) descend = false;
       if (descend) { cur = nearRef; continue; }
     }
     // pop (RT:348), skipping subtrees that start beyond the current closest hit
@@ -151,7 +158,7 @@ RTD void trace(const KParams& P, f3 o, f3 d, bool anyhit, bool cull, int* __rest
       --sp;
       int r = sref[sp * stride];
       float dd = sdist[sp * stride];
-      if (cull && dd > cull_limit(best)) continue;
+      if (cull && dd > cull_limit(best, P.cull_eps, inv.x, inv.y, inv.z)) continue;
       cur = r;
       found = true;
       break;

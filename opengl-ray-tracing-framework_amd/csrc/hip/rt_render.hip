@@ -37,6 +37,7 @@ struct rt_ctx {
   float4* d_trin = nullptr;
   float4* d_mats = nullptr;
   int n_tri = 0, n_mats = 0, root = 0, has_scene = 0, stack_entries = 2;
+  double cull_R = 0.0, cull_K = 0.0, cull_off = 0.0;  // culling bound of the scene (cull_bound_stats)
   bool scene_set = false;
   std::vector<int32_t> tri_mat;  // host copy of the per-triangle material ids (for updates)
   std::vector<float> mat_table;  // host copy, 32 floats per material
@@ -122,6 +123,56 @@ inline void geometric_normal(const float* p1, const float* p2, const float* p3, 
   float cx = ay * bz - by * az, cy = az * bx - bz * ax, cz = ax * by - bx * ay;
   float inv = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);
   n[0] = cx * inv; n[1] = cy * inv; n[2] = cz * inv;
+}
+
+// Culling bound ("What the culling margin covers").  A subtree may be skipped when
+// its box entry t0 exceeds the best hit; that is exact only if no triangle inside the box can be
+// accepted by the reference's test (RT:241-299) at a computed t below t0.  An accepted hit point
+// P = S + d*t (fp32) lies within eps (per axis) of its triangle, hence of every box holding it:
+//   off-plane |(P - p1).N| <= 36 u R  (rounding of RT:265 and of P; R bounds |coords|, origins),
+//   in-plane slack of the three edge signs <= 70 u R / cos(theta)  (theta: fp32 N vs exact normal),
+//   X = S + d*t (exact) vs P: <= 8 u R,
+//   + the triangle's vertices off the plane (p1, N): max_k |(pk - p1).N|,
+// so t >= t0 - eps * max|1/d_a|.  Returned per scene: K (units of u R) and off; the render
+// doubles eps = K u R + off as safety.  Degenerate (zero-area with a finite fp32 normal) or badly
+// conditioned triangles, or triangles outside their leaf box, give K = inf: no culling.
+struct CullStats {
+  double R = 0.0, K = 0.0, off = 0.0;
+};
+CullStats cull_bound_stats(const rt_scene_soa* s) {
+  CullStats cs;
+  const int nt = s->n_triangles;
+  for (int i = 0; i < nt; i++) {
+    const float* p[3] = {s->p1 + 3 * i, s->p2 + 3 * i, s->p3 + 3 * i};
+    float ng[3];
+    geometric_normal(p[0], p[1], p[2], ng);
+    for (int k = 0; k < 3; k++)
+      for (int a = 0; a < 3; a++) cs.R = std::max(cs.R, std::fabs((double)p[k][a]));
+    if (!(std::isfinite(ng[0]) && std::isfinite(ng[1]) && std::isfinite(ng[2]))) continue;  // never hit (NaN tests)
+    double e1[3], e2[3], cx[3];
+    for (int a = 0; a < 3; a++) { e1[a] = (double)p[1][a] - p[0][a]; e2[a] = (double)p[2][a] - p[0][a]; }
+    cx[0] = e1[1] * e2[2] - e1[2] * e2[1];
+    cx[1] = e1[2] * e2[0] - e1[0] * e2[2];
+    cx[2] = e1[0] * e2[1] - e1[1] * e2[0];
+    const double nrm = std::sqrt(cx[0] * cx[0] + cx[1] * cx[1] + cx[2] * cx[2]);
+    const double cosT = nrm > 0.0 ? (ng[0] * cx[0] + ng[1] * cx[1] + ng[2] * cx[2]) / nrm : 0.0;
+    if (!(cosT > 0.25)) { cs.K = INFINITY; continue; }
+    cs.K = std::max(cs.K, 44.0 + 70.0 / cosT);
+    for (int k = 1; k < 3; k++) {
+      double o = 0.0;
+      for (int a = 0; a < 3; a++) o += ((double)p[k][a] - p[0][a]) * ng[a];
+      cs.off = std::max(cs.off, std::fabs(o));
+    }
+  }
+  // every leaf's triangles inside the leaf's box (the reference's own boxes are their min/max)
+  for (int n = 1; n < s->n_nodes && s->node_n; n++) {
+    if (s->node_n[n] <= 0) continue;
+    for (int i = s->node_index[n]; i < s->node_index[n] + s->node_n[n] && i < nt; i++)
+      for (const float* q : {s->p1 + 3 * i, s->p2 + 3 * i, s->p3 + 3 * i})
+        for (int a = 0; a < 3; a++)
+          if (!(q[a] >= s->node_aa[3 * n + a] && q[a] <= s->node_bb[3 * n + a])) cs.K = INFINITY;
+  }
+  return cs;
 }
 
 // Material.h fields -> 32-float device entry; ax/ay by getMaterial's formula (RT:205-207).
@@ -764,6 +815,10 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
   c->n_mats = s->n_materials;
   c->root = root;
   c->has_scene = has;
+  {
+    const CullStats cs = cull_bound_stats(s);
+    c->cull_R = cs.R; c->cull_K = cs.K; c->cull_off = cs.off;
+  }
   c->stack_entries = std::max(2, depth + 1);
   c->wide = wide;
   c->qroot = qroot;
@@ -1024,6 +1079,17 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
     P.qnodes = c->d_qnodes; P.qroot = c->qroot;
+    {  // eps of the culling bound for this call's origins (camera position, scene points)
+      double R = c->cull_R;
+      for (int a = 0; a < 3; a++) R = std::max(R, std::fabs((double)fp->position[a]));
+      // x (1 + 2^-9): the fp32 rounding of eps * max|1/d| and of the sum in cull_limit
+      const double eps = 2.0 * (c->cull_K * 0x1p-24 * R * (1.0 + 0x1p-10) + c->cull_off) * (1.0 + 0x1p-9);
+      // RT_CULL_EPS_SCALE (tests only): 0 restores the round-1 heuristic margin, whose hole
+      // tests/test_gpu_cull.py demonstrates
+      const char* es = getenv("RT_CULL_EPS_SCALE");
+      const double sc = es ? atof(es) : 1.0;
+      P.cull_eps = (eps * sc < 1e30) ? (float)(eps * sc) : INFINITY;
+    }
     P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
     P.hdr = c->d_hdr; P.cache = c->d_cache; P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;

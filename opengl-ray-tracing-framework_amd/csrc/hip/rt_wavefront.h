@@ -366,8 +366,8 @@ RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
 }
 
 // pop the next surviving subtree (RT:348); false when the stack is exhausted
-RTD bool tl_pop(TraceLane& L, const TraceStack& S, bool cull) {
-  const float lim = cull_limit(L.best);
+RTD bool tl_pop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+  const float lim = cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz);
   while (L.sp > 0) {
     --L.sp;
     const int2 ent = L.sp < S.KL ? S.lds[L.sp * TL_LANES] : unpack_ent(S.ovf[(size_t)(L.sp - S.KL) * S.ovs]);
@@ -400,9 +400,9 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
   } else if (d2 > 0) {
     nearRef = ref.y; nearE = e2; descend = true;
   }
-  if (descend && cull && nearE > cull_limit(L.best)) descend = false;
+  if (descend && cull && nearE > cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz)) descend = false;
   L.cur = nearRef;
-  L.haveCur = descend || tl_pop(L, S, cull);
+  L.haveCur = descend || tl_pop(P, L, S, cull);
 }
 
 // 4-wide node L.cur: the four (grand)child boxes of the binary subtree it replaces, each with
@@ -412,7 +412,7 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   // t0 / t1 of RT:312-313 for the four children; the box is hit iff t1 >= t0 && t1 > 0,
   // which is exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
   const int4 rf = ld<int4>(P.qnodes, off + 96u);
-  const float lim = cull ? cull_limit(L.best) : __int_as_float(0x7f800000);
+  const float lim = cull ? cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz) : __int_as_float(0x7f800000);
   float k[4];
   int r[4];
   auto keep = [&](int c, float t0, float t1, int ref) {
@@ -484,7 +484,7 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
     if (r[1] != Q_EMPTY) tl_push(L, S, e1);
   }
   L.cur = r[0];
-  L.haveCur = r[0] != Q_EMPTY || tl_pop(L, S, cull);
+  L.haveCur = r[0] != Q_EMPTY || tl_pop(P, L, S, cull);
 }
 
 #ifndef RT_TRACE_WPE
@@ -643,7 +643,7 @@ void wf_trace(const WFParams W) {
               if (COUNT) { v_leaf++; v_park++; }
               L.tri_i = leaf_first(L.cur);
               L.tri_end = L.tri_i + leaf_count(L.cur);
-              L.haveCur = tl_pop(L, TS, cull);
+              L.haveCur = tl_pop(P, L, TS, cull);
             }
           } else {
             if (COUNT) { v_int++; ray_steps++; }
@@ -671,7 +671,7 @@ void wf_trace(const WFParams W) {
           }
         }
         if (!finished && !L.haveCur && L.tri_i >= L.tri_end) {
-          L.haveCur = tl_pop(L, TS, cull);
+          L.haveCur = tl_pop(P, L, TS, cull);
           if (!L.haveCur) finished = true;
         }
       }
@@ -693,7 +693,7 @@ void wf_trace(const WFParams W) {
             parked = L.cur;
             haveParked = true;
             if (MODE == TM_WW) L.haveCur = false;
-            else L.haveCur = tl_pop(L, TS, cull);
+            else L.haveCur = tl_pop(P, L, TS, cull);
           } else {
             if (COUNT) { v_int++; ray_steps++; }
             if (WIDE) tl_qnode(P, L, TS, cull);
@@ -719,7 +719,7 @@ void wf_trace(const WFParams W) {
         }
       }
       if (busy && !finished && !L.haveCur) {
-        L.haveCur = tl_pop(L, TS, cull);
+        L.haveCur = tl_pop(P, L, TS, cull);
         if (!L.haveCur) finished = true;
       }
     }
