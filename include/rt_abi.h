@@ -49,9 +49,10 @@ enum {
   RT_ERR_LIMIT = -6     /* scene exceeds a kernel limit (leaf > 16 tris, depth > 64) */
 };
 
-/* Frames per kernel batch; the path-state budget (208 B per pixel-frame, RT_MAX_SLOTS, default
- * 320Mi slots = 69 GB) bounds it too: 161 frames at 1920x1080 on one GPU, all 512 of a bench
- * step on each of 8 tile-sharded GPUs. */
+/* Frames per kernel batch; the path-state budget (208 B per pixel-frame; rt_set_max_paths or
+ * RT_MAX_SLOTS, default 320 Mi slots = 70 GB) bounds it too: 161 frames at 1920x1080 with the
+ * default budget; bench.py raises the budget to a whole 1024-frame step, which one GPU runs as two
+ * launches of 512 frames (229 GB) and each of 8 tile-sharded GPUs as one launch (57 GB). */
 enum { RT_MAX_FRAMES_PER_LAUNCH = 1024 };
 
 /* Disney material (src/core/Material.h:25-46), 24 floats, same layout as rts_material. */
