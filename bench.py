@@ -74,6 +74,8 @@ def parse_args(argv=None):
     ap.add_argument("--single-frames", type=int, default=64,
                     help="frames rendered one per rt_render call after the timed region (ms_per_frame_single)")
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="N > 1: keep the interleaved t %% N tile map instead of the cost-balanced one")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launcher, frame plan, tiling and the gloo gather only (CPU tests)")
     return ap.parse_args(argv)
@@ -225,8 +227,18 @@ def dry_run(args, rank: int, world: int) -> int:
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     ro = cf.rand_origins(total_frames)
-    mine = tiling.local_tiles(W, H, args.tile, args.tile, rank, world)
-    mlt = tiling.max_local_tiles(W, H, args.tile, args.tile, world)
+    owner = None
+    if world > 1 and not args.no_balance:
+        # the GPU run measures per-tile costs with rt_tile_costs; here a synthetic stand-in
+        # through the same exchange (all_reduce of each rank's share) and the same balance()
+        n_t = len(tiling.modulo_owners(W, H, args.tile, args.tile, world))
+        full = torch.zeros(n_t, dtype=torch.int64)
+        for t in tiling.local_tiles(W, H, args.tile, args.tile, rank, world):
+            full[t] = (t * 7919) % 1000 + 1
+        dist.all_reduce(full)
+        owner = tiling.balance(full.numpy(), world)
+    mine = tiling.local_tiles(W, H, args.tile, args.tile, rank, world, owner)
+    mlt = tiling.max_local_tiles(W, H, args.tile, args.tile, world, owner)
     px = sum(tiling.tile_rect(t, W, H, args.tile, args.tile)[2] * tiling.tile_rect(t, W, H, args.tile, args.tile)[3]
              for t in mine)
     t0 = time.perf_counter()
@@ -247,6 +259,7 @@ def dry_run(args, rank: int, world: int) -> int:
                           "warmup": warm, "dry_run": True, "frames_planned": total_frames,
                           "rand_origin_last": float(ro[-1]), "pixels_covered": total_px,
                           "frame_pixels": W * H, "gather_ok": bool(ok),
+                          "tile_assignment": "modulo" if owner is None else "cost-balanced",
                           "gather_ms": round(float(elapsed[0]) * 1e3, 3)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -297,6 +310,19 @@ def main(argv=None) -> int:
     r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(*env)
     r.resize(W, H, tile=args.tile, rank=rank, world=world)
+    balanced = world > 1 and not args.no_balance
+    if balanced:
+        # tiles assigned by a cost estimate from one probe frame.  Every rank measures
+        # its interleaved share (rt_tile_costs: node + triangle steps per tile), the shares are
+        # summed into the full cost vector, and every rank derives the same LPT owner map
+        from rtamd import tiling
+        n_t = len(tiling.modulo_owners(W, H, args.tile, args.tile, world))
+        full = torch.zeros(n_t, dtype=torch.int64, device="cuda")
+        mine = torch.tensor(tiling.local_tiles(W, H, args.tile, args.tile, rank, world), dtype=torch.int64,
+                            device="cuda")
+        full[mine] = torch.from_numpy(r.tile_costs(fp, ro[-1:]).astype(np.int64)).to("cuda")
+        dist.all_reduce(full)
+        r.set_tile_owners(tiling.balance(full.cpu().numpy(), world))
     ad = r.accum_device()
     # path-state budget: a whole step's frames in flight at once (208 B per pixel-frame: 57 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
@@ -406,6 +432,7 @@ def main(argv=None) -> int:
                    "width": W, "height": H, "frames_per_step": F, "spp_timed": steps * F,
                    "tile": args.tile, "path_slots_per_rank": path_slots,
                    "parallelism": f"pixel-tiles x{world} + frame-end gather",
+                   "tile_assignment": "cost-balanced (rt_tile_costs probe frame)" if balanced else "interleaved t % N",
                    "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
         "kernel": {"name": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "launches": st["trace_launches"],
                    "render_call_ms": round(launch_ms, 4), "render_calls": st["launches"],

@@ -133,6 +133,17 @@ int rt_set_loop_num(rt_ctx* ctx, int32_t loop_num);
 int rt_get_loop_num(const rt_ctx* ctx, int32_t* loop_num);
 /* Clear this rank's accumulation to zero (fresh FBO contents). */
 int rt_clear_accum(rt_ctx* ctx);
+/* Tile ownership (SURVEY §8(e) "by a cost estimate from frame 1"): owner[t] = the rank that renders
+ * global tile t (row-major from the bottom-left, n_tiles = tiles_x * tiles_y of the rt_resize
+ * tiling).  rt_resize sets owner[t] = t % world; every rank of a job must set the same map.  Local
+ * order = ascending tile id.  Re-sizes the accumulation (zeroed) and the pixel list, resets LoopNum. */
+int rt_set_tile_owners(rt_ctx* ctx, const int32_t* owner, int32_t n_tiles);
+int rt_get_tile_owners(const rt_ctx* ctx, int32_t* owner, int32_t n_tiles);
+/* Cost probe for rt_set_tile_owners: renders n_frames and returns, per LOCAL tile of this ctx,
+ * its rays' BVH node + triangle steps plus a per-ray share (deterministic integers).  LoopNum and
+ * the accumulation are left as they were; the stats counters include the probe frames. */
+int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
+                  uint64_t* costs);
 /* Path-state budget in pixel-frames (208 B each): frames in flight per launch = slots / pixels of
  * this rank, at most RT_MAX_FRAMES_PER_LAUNCH.  0 = RT_MAX_SLOTS from the environment or the
  * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL

@@ -29,6 +29,14 @@
 #define GM_FN static inline
 #endif
 
+// RT_HW_MATH (measurement builds only, never the parity target): device code uses the
+// hardware / ocml transcendentals instead of the polynomials below, to price the bit-exact ones
+#if defined(RT_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
+#define GM_HW 1
+#else
+#define GM_HW 0
+#endif
+
 namespace gm {
 
 GM_FN uint32_t fbits(float f) { union { float f; uint32_t u; } v; v.f = f; return v.u; }
@@ -60,6 +68,10 @@ GM_FN float exp2i_(int n) { return bitsf((uint32_t)(n + 127) << 23); }
 #define GM_2OPI   0.636619746685028076171875f
 
 GM_FN void sincos_(float x, float* s_out, float* c_out) {
+#if GM_HW
+  __sincosf(x, s_out, c_out);
+  return;
+#endif
   float j = rint_(x * GM_2OPI);
   float r = x - j * GM_PIO2_1;
   r = r - j * GM_PIO2_2;
@@ -100,6 +112,9 @@ GM_FN float atan_pos_(float t) {
 
 // GLSL atan(y, x): quadrant-correct arctangent (C atan2 conventions for zeros).
 GM_FN float atan2_(float y, float x) {
+#if GM_HW
+  return atan2f(y, x);
+#endif
   if (isnan_(x) || isnan_(y)) return x + y;
   float ax = fabs_(x), ay = fabs_(y);
   float a;
@@ -113,6 +128,9 @@ GM_FN float atan2_(float y, float x) {
 
 // ---- asin -----------------------------------------------------------------------
 GM_FN float asin_(float x) {
+#if GM_HW
+  return asinf(x);
+#endif
   float a = fabs_(x);
   if (!(a <= 1.0f)) return (x - x) / (x - x);  // NaN (also for NaN input)
   float z, s;
@@ -128,6 +146,9 @@ GM_FN float asin_(float x) {
 // ---- exp / log / pow ------------------------------------------------------------
 #define GM_LOG2EF 1.44269504088896341f
 GM_FN float exp_(float x) {
+#if GM_HW
+  return __expf(x);
+#endif
   if (isnan_(x)) return x;
   if (x > 88.72283905206835f) return bitsf(0x7f800000u);
   if (x < -103.972077083991796f) return 0.0f;
@@ -144,6 +165,9 @@ GM_FN float exp_(float x) {
 }
 
 GM_FN float log_(float x) {
+#if GM_HW
+  return __logf(x);
+#endif
   if (isnan_(x)) return x;
   if (x < 0.0f) return (x - x) / (x - x);
   if (x == 0.0f) return bitsf(0xff800000u);
@@ -169,6 +193,9 @@ GM_FN float log_(float x) {
 
 // GLSL pow(x, y) (spec: exp2(y * log2(x)); undefined for x < 0).
 GM_FN float pow_(float x, float y) {
+#if GM_HW
+  return __powf(x, y);
+#endif
   if (y == 0.0f) return 1.0f;
   if (x == 1.0f) return 1.0f;
   return exp_(y * log_(x));

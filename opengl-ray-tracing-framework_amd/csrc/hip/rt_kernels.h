@@ -37,6 +37,8 @@ struct KParams {
   const float* __restrict__ rand_origin;  // per frame of this launch (device table)
   const float2* __restrict__ sobol;       // per frame of this launch: sobolVec2 of bounces 0..3 (wf_sobol)
   int W, H, tile_w, tile_h, tiles_x, rank, world;
+  const int* __restrict__ tile_ids;   // global tile id of each local tile (rt_set_tile_owners)
+  unsigned long long* __restrict__ tile_cost;  // rt_tile_costs probe: per local tile (else null)
   unsigned int n_work;
   const GNode* __restrict__ nodes;  // binary tree; GNode.ref.z = DFS rank of the first leaf on the right
   int root, has_scene, stack_entries;
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(256) void rt_path_kernel(const KParams P) {
         if (my < P.n_work) {
           int lt = (int)(my / (unsigned)tpx);
           int r = (int)(my - (unsigned)lt * (unsigned)tpx);
-          int gt = P.rank + lt * P.world;
+          int gt = P.tile_ids[lt];
           int tx = gt % P.tiles_x, ty = gt / P.tiles_x;
           int blk = r >> 6, in = r & 63;
           int bxs = P.tile_w >> 3;
@@ -431,14 +433,17 @@ __global__ __launch_bounds__(256) void rt_path_kernel(const KParams P) {
 }
 
 // Un-permute rank-major gathered tile buffers into a W x H x 3 fp32 frame.
+// tile_src[global tile] = (owning rank, its local index there).
 __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, float* __restrict__ frame, int W, int H,
-                                   int tile_w, int tile_h, int tiles_x, int world, int max_local_tiles) {
+                                   int tile_w, int tile_h, int tiles_x, const int2* __restrict__ tile_src,
+                                   int max_local_tiles) {
   int px = blockIdx.x * blockDim.x + threadIdx.x;
   int py = blockIdx.y;
   if (px >= W || py >= H) return;
   int tx = px / tile_w, ty = py / tile_h;
   int gt = ty * tiles_x + tx;
-  int rank = gt % world, lt = gt / world;
+  const int2 src = tile_src[gt];
+  int rank = src.x, lt = src.y;
   int lx = px - tx * tile_w, ly = py - ty * tile_h;
   size_t idx = ((size_t)rank * max_local_tiles + lt) * (size_t)(tile_w * tile_h) + (size_t)ly * tile_w + lx;
   float4 c = gathered[idx];

@@ -91,6 +91,13 @@ struct rt_ctx {
   rtd::WFState wfg[MAX_GROUPS]{};
   hipStream_t aux[MAX_GROUPS] = {};
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
+  // tile ownership: owner[t] = rank of global tile t (default t % world; rt_set_tile_owners);
+  // my_tiles = this rank's global tiles in local order; tile_src[t] = (rank, local index)
+  std::vector<int32_t> owner, my_tiles;
+  int* d_tile_ids = nullptr;       // my_tiles on the device (KParams.tile_ids)
+  int2* d_tile_src = nullptr;      // tile_src on the device (rt_assemble_kernel)
+  unsigned long long* d_tile_cost = nullptr;  // rt_tile_costs: per local tile, during the probe only
+  bool tile_cost_on = false;
   float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera)
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
@@ -687,6 +694,9 @@ int rt_destroy(rt_ctx* c) {
   if (c->h_ftab) (void)hipHostFree(c->h_ftab);
   dfree(c->d_ftab);
   dfree(c->d_pix);
+  dfree(c->d_tile_ids);
+  dfree(c->d_tile_src);
+  dfree(c->d_tile_cost);
   dfree(c->d_cam);
   dfree(c->d_stack_ovf);
   dfree(c->d_disp);
@@ -914,13 +924,10 @@ int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32
   return RT_OK;
 }
 
-int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
-  if (!c || width <= 0 || height <= 0) return RT_ERR_ARG;
-  rt_tiling tl = t ? *t : rt_tiling{32, 32, 0, 1};
-  if (tl.tile_w <= 0 || tl.tile_h <= 0 || (tl.tile_w % 8) || (tl.tile_h % 8) || tl.world <= 0 || tl.rank < 0 ||
-      tl.rank >= tl.world)
-    return fail(c, RT_ERR_ARG, "bad tiling (tile sizes must be positive multiples of 8, 0 <= rank < world)");
-  if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
+// (Re)build everything that depends on the tiling: the tile tables, the accumulation buffer
+// (zeroed), this rank's pixel list (its tiles in local order, 8x8 blocks inside a tile: ray
+// coherence) and the wavefront state sized for it.
+static int apply_tiling(rt_ctx* c, int width, int height, const rt_tiling& tl, std::vector<int32_t> owner) {
   HIPCHK(c, hipSetDevice(c->device));
   // the old pixel lists / accumulation no longer describe the frame from here on: a failure
   // below leaves the context un-sized (rt_render_async then refuses) rather than half-resized
@@ -929,18 +936,33 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   c->tile_w = tl.tile_w; c->tile_h = tl.tile_h; c->rank = tl.rank; c->world = tl.world;
   c->tiles_x = (width + tl.tile_w - 1) / tl.tile_w;
   c->tiles_y = (height + tl.tile_h - 1) / tl.tile_h;
-  int total = c->tiles_x * c->tiles_y;
-  c->local_tiles = total > tl.rank ? (total - tl.rank + tl.world - 1) / tl.world : 0;
-  c->max_local_tiles = (total + tl.world - 1) / tl.world;
+  const int total = c->tiles_x * c->tiles_y;
+  std::vector<int> count(tl.world, 0);
+  std::vector<int2> src(total);
+  c->my_tiles.clear();
+  for (int t = 0; t < total; t++) {
+    src[t] = make_int2(owner[t], count[owner[t]]++);
+    if (owner[t] == tl.rank) c->my_tiles.push_back(t);
+  }
+  c->owner = std::move(owner);
+  c->local_tiles = (int)c->my_tiles.size();
+  c->max_local_tiles = *std::max_element(count.begin(), count.end());
   dfree(c->d_accum);
   size_t bytes = (size_t)std::max(1, c->max_local_tiles) * tl.tile_w * tl.tile_h * sizeof(float4);
   HIPCHK(c, hipMalloc(&c->d_accum, bytes));
   HIPCHK(c, hipMemset(c->d_accum, 0, bytes));
-  // pixel list of this rank: its tiles in order, 8x8 blocks inside a tile (ray coherence)
+  dfree(c->d_tile_ids);
+  dfree(c->d_tile_src);
+  dfree(c->d_tile_cost);
+  HIPCHK(c, hipMalloc(&c->d_tile_ids, std::max<size_t>(1, c->my_tiles.size()) * sizeof(int)));
+  HIPCHK(c, hipMalloc(&c->d_tile_src, std::max<size_t>(1, src.size()) * sizeof(int2)));
+  if (!c->my_tiles.empty())
+    HIPCHK(c, hipMemcpy(c->d_tile_ids, c->my_tiles.data(), c->my_tiles.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (!src.empty()) HIPCHK(c, hipMemcpy(c->d_tile_src, src.data(), src.size() * sizeof(int2), hipMemcpyHostToDevice));
   std::vector<unsigned int> xy, acc;
   const int tpx = tl.tile_w * tl.tile_h;
   for (int lt = 0; lt < c->local_tiles; lt++) {
-    const int gt = tl.rank + lt * tl.world;
+    const int gt = c->my_tiles[lt];
     const int tx = gt % c->tiles_x, ty = gt / c->tiles_x;
     for (int r = 0; r < tpx; r++) {
       const int blk = r >> 6, in = r & 63, bxs = tl.tile_w >> 3;
@@ -969,6 +991,37 @@ int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
   c->wf.cam = c->d_cam;
   c->frame_set = true;
   c->loop_num = 0;
+  return RT_OK;
+}
+
+int rt_resize(rt_ctx* c, int32_t width, int32_t height, const rt_tiling* t) {
+  if (!c || width <= 0 || height <= 0) return RT_ERR_ARG;
+  rt_tiling tl = t ? *t : rt_tiling{32, 32, 0, 1};
+  if (tl.tile_w <= 0 || tl.tile_h <= 0 || (tl.tile_w % 8) || (tl.tile_h % 8) || tl.world <= 0 || tl.rank < 0 ||
+      tl.rank >= tl.world)
+    return fail(c, RT_ERR_ARG, "bad tiling (tile sizes must be positive multiples of 8, 0 <= rank < world)");
+  if (width > 65535 || height > 65535) return fail(c, RT_ERR_LIMIT, "frame larger than 65535");
+  const int total = ((width + tl.tile_w - 1) / tl.tile_w) * ((height + tl.tile_h - 1) / tl.tile_h);
+  std::vector<int32_t> owner(total);
+  for (int g = 0; g < total; g++) owner[g] = g % tl.world;  // interleaved default
+  return apply_tiling(c, width, height, tl, std::move(owner));
+}
+
+int rt_set_tile_owners(rt_ctx* c, const int32_t* owner, int32_t n_tiles) {
+  if (!c || !owner || n_tiles <= 0) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  if (n_tiles != c->tiles_x * c->tiles_y) return fail(c, RT_ERR_ARG, "n_tiles differs from the frame's tile count");
+  for (int g = 0; g < n_tiles; g++)
+    if (owner[g] < 0 || owner[g] >= c->world) return fail(c, RT_ERR_ARG, "tile owner outside [0, world)");
+  const rt_tiling tl{c->tile_w, c->tile_h, c->rank, c->world};
+  return apply_tiling(c, c->W, c->H, tl, std::vector<int32_t>(owner, owner + n_tiles));
+}
+
+int rt_get_tile_owners(const rt_ctx* c, int32_t* owner, int32_t n_tiles) {
+  if (!c || !owner) return RT_ERR_ARG;
+  if (!c->frame_set) return RT_ERR_STATE;
+  if (n_tiles != (int32_t)c->owner.size()) return RT_ERR_ARG;
+  memcpy(owner, c->owner.data(), c->owner.size() * sizeof(int32_t));
   return RT_OK;
 }
 
@@ -1075,7 +1128,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.env_intensity = fp->env_intensity; P.env_angle = fp->env_angle;
     P.max_bounce = fp->max_bounce; P.flags = fp->flags; P.n_frames = nf;
     P.W = c->W; P.H = c->H; P.tile_w = c->tile_w; P.tile_h = c->tile_h; P.tiles_x = c->tiles_x;
-    P.rank = c->rank; P.world = c->world;
+    P.rank = c->rank; P.world = c->world; P.tile_ids = c->d_tile_ids;
+    P.tile_cost = c->tile_cost_on ? c->d_tile_cost : nullptr;
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
     P.qnodes = c->d_qnodes; P.qroot = c->qroot;
@@ -1334,6 +1388,45 @@ int rt_stats_reset(rt_ctx* c) {
   return RT_OK;
 }
 
+// Per-tile cost probe for a balanced tile assignment (rt_set_tile_owners): renders n_frames with
+// the visit-counting trace, which adds every ray's node + triangle steps (+ RT_COST_PER_RAY) to
+// its tile's counter.  Integer counts of a deterministic render: the same on every rank and box.
+// LoopNum and the accumulation are restored afterwards; the stats counters include the probe.
+int rt_tile_costs(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, uint64_t* costs) {
+  if (!c || !fp || !rand_origin || !costs || n_frames <= 0) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  if (c->local_tiles == 0) return RT_OK;
+  int rc = rt_synchronize(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t abytes = (size_t)std::max(1, c->max_local_tiles) * c->tile_w * c->tile_h * sizeof(float4);
+  void* saved = nullptr;
+  HIPCHK(c, hipMalloc(&saved, abytes));
+  HIPCHK(c, hipMemcpy(saved, c->d_accum, abytes, hipMemcpyDeviceToDevice));
+  const int loop = c->loop_num;
+  dfree(c->d_tile_cost);
+  hipError_t he = hipMalloc(&c->d_tile_cost, (size_t)c->local_tiles * sizeof(unsigned long long));
+  if (he == hipSuccess) he = hipMemset(c->d_tile_cost, 0, (size_t)c->local_tiles * sizeof(unsigned long long));
+  if (he != hipSuccess) {
+    (void)hipFree(saved);
+    return fail(c, RT_ERR_HIP, std::string("rt_tile_costs: ") + hipGetErrorString(he));
+  }
+  rt_frame_params q = *fp;
+  q.flags = (q.flags | RT_FLAG_COUNT_VISITS) & ~RT_FLAG_MEGAKERNEL;
+  c->tile_cost_on = true;
+  rc = rt_render(c, &q, rand_origin, n_frames, nullptr);
+  c->tile_cost_on = false;
+  if (rc == RT_OK) {
+    he = hipMemcpy(costs, c->d_tile_cost, (size_t)c->local_tiles * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (he == hipSuccess) he = hipMemcpy(c->d_accum, saved, abytes, hipMemcpyDeviceToDevice);
+    if (he != hipSuccess) rc = fail(c, RT_ERR_HIP, std::string("rt_tile_costs: ") + hipGetErrorString(he));
+  }
+  (void)hipFree(saved);
+  dfree(c->d_tile_cost);
+  c->loop_num = loop;
+  return rc;
+}
+
 int rt_render(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, rt_stats* st) {
   int rc = rt_render_async(c, fp, rand_origin, n_frames);
   if (rc) return rc;
@@ -1392,7 +1485,7 @@ static int accum_transfer(rt_ctx* c, float* host, int32_t layout, bool to_host) 
   std::vector<float4> buf((size_t)std::max(1, c->max_local_tiles) * tpx);
   HIPCHK(c, hipMemcpy(buf.data(), c->d_accum, buf.size() * sizeof(float4), hipMemcpyDeviceToHost));
   for (int lt = 0; lt < c->local_tiles; lt++) {
-    int gt = c->rank + lt * c->world;
+    int gt = c->my_tiles[lt];
     int tx = gt % c->tiles_x, ty = gt / c->tiles_x;
     for (int ly = 0; ly < c->tile_h; ly++)
       for (int lx = 0; lx < c->tile_w; lx++) {
@@ -1445,7 +1538,7 @@ int rt_assemble_frame(rt_ctx* c, const void* gathered, int32_t world, void* fram
   HIPCHK(c, hipSetDevice(c->device));
   dim3 block(256), grid((c->W + 255) / 256, c->H);
   hipLaunchKernelGGL(rtd::rt_assemble_kernel, grid, block, 0, c->stream, (const float4*)gathered, (float*)frame, c->W,
-                     c->H, c->tile_w, c->tile_h, c->tiles_x, world, std::max(1, c->max_local_tiles));
+                     c->H, c->tile_w, c->tile_h, c->tiles_x, (const int2*)c->d_tile_src, std::max(1, c->max_local_tiles));
   HIPCHK(c, hipGetLastError());
   return RT_OK;
 }
@@ -1459,7 +1552,7 @@ int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb) {
     if (!c->frame_set) return fail(c0, RT_ERR_STATE, "rt_gather: rt_resize every context first");
     if (c->rank != r || c->world != n) return fail(c0, RT_ERR_ARG, "rt_gather: ctxs[r] must render rank r of a world of n");
     if (c->W != c0->W || c->H != c0->H || c->tile_w != c0->tile_w || c->tile_h != c0->tile_h ||
-        c->max_local_tiles != c0->max_local_tiles)
+        c->max_local_tiles != c0->max_local_tiles || c->owner != c0->owner)
       return fail(c0, RT_ERR_ARG, "rt_gather: contexts differ in frame size or tiling");
   }
   const size_t part = (size_t)std::max(1, c0->max_local_tiles) * c0->tile_w * c0->tile_h * sizeof(float4);

@@ -81,7 +81,7 @@ RTD bool work_pixel(const KParams& P, unsigned int w, int& px, int& py, int& acc
   const int tpx = P.tile_w * P.tile_h;
   int lt = (int)(w / (unsigned)tpx);
   int r = (int)(w - (unsigned)lt * (unsigned)tpx);
-  int gt = P.rank + lt * P.world;
+  int gt = P.tile_ids[lt];
   int tx = gt % P.tiles_x, ty = gt / P.tiles_x;
   int blk = r >> 6, in = r & 63;
   int bxs = P.tile_w >> 3;
@@ -490,6 +490,9 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 1
 #endif
+#ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
+#define RT_COST_PER_RAY 16u
+#endif
 #ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s;
                        // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%;
                        // final build: 20 / 24 / 28 -> +0.3% / 0 / -0.9%
@@ -725,7 +728,14 @@ void wf_trace(const WFParams W) {
     }
     if (busy && finished) {
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
-      if (COUNT) { ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; v_rays++; }
+      if (COUNT) {
+        if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
+          const unsigned int w = (unsigned int)(entry >> 1) / (unsigned int)P.n_frames;
+          atomicAdd(&P.tile_cost[S.pix_acc[w] / (unsigned int)(P.tile_w * P.tile_h)],
+                    (unsigned long long)(ray_steps + RT_COST_PER_RAY));
+        }
+        ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; v_rays++;
+      }
       busy = false;
     }
   }

@@ -33,7 +33,8 @@ ABI_SYMBOLS = (
     "rt_update_materials", "rt_set_env", "rt_resize", "rt_reset", "rt_set_loop_num", "rt_get_loop_num",
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
-    "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather",
+    "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
+    "rt_tile_costs",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -174,6 +175,9 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
     L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
     L.rt_set_max_paths.argtypes = [vp, C.c_uint64]
+    L.rt_set_tile_owners.argtypes = [vp, _i32p, C.c_int32]
+    L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
+    L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
     L.rt_gather.argtypes = [C.POINTER(vp), C.c_int32, _f32p]
     return L
 
@@ -271,6 +275,28 @@ class Renderer:
         self._check(self._L.rt_resize(self._h, width, height, C.byref(t)), "rt_resize")
         self.width, self.height = width, height
         self.tiling = (tile, tile, rank, world)
+
+    def set_tile_owners(self, owner: Sequence[int]) -> None:
+        """owner[t] = rank rendering global tile t (rt_set_tile_owners; every rank sets the same map)."""
+        o = np.ascontiguousarray(owner, np.int32)
+        self._check(self._L.rt_set_tile_owners(self._h, o.ctypes.data_as(_i32p), len(o)), "rt_set_tile_owners")
+
+    def tile_owners(self) -> np.ndarray:
+        tx = (self.width + self.tiling[0] - 1) // self.tiling[0]
+        ty = (self.height + self.tiling[1] - 1) // self.tiling[1]
+        o = np.zeros(tx * ty, np.int32)
+        self._check(self._L.rt_get_tile_owners(self._h, o.ctypes.data_as(_i32p), len(o)), "rt_get_tile_owners")
+        return o
+
+    def tile_costs(self, params: FrameParams, rand_origins: Sequence[float]) -> np.ndarray:
+        """Per local tile cost of rendering these frames (rt_tile_costs; state left unchanged)."""
+        ro = np.ascontiguousarray(rand_origins, np.float32)
+        p = params.to_c()
+        n = self.accum_device()["local_tiles"]
+        out = np.zeros(max(1, n), np.uint64)
+        self._check(self._L.rt_tile_costs(self._h, C.byref(p), _fp(ro), len(ro),
+                                          out.ctypes.data_as(C.POINTER(C.c_uint64))), "rt_tile_costs")
+        return out[:n]
 
     # ------------------------------------------------------------------ frames
     def reset(self) -> None:

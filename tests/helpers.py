@@ -15,13 +15,15 @@ def oracle_render(sd, env, W, H, frames, accum=None, x0=0, y0=0, w=None, h=None)
     return orc.render(scene, frames, W, H, x0=x0, y0=y0, w=w, h=h, accum=accum)
 
 
-def gpu_render(r, sd, env, W, H, fp, ro, tile=32, rank=0, world=1, encoded=False, accum=None, loop_num=0):
+def gpu_render(r, sd, env, W, H, fp, ro, tile=32, rank=0, world=1, encoded=False, accum=None, loop_num=0, owner=None):
     if encoded:
         r.set_scene_encoded(sd.tri_enc, sd.node_enc)
     else:
         r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(env[0], env[1])
     r.resize(W, H, tile=tile, rank=rank, world=world)
+    if owner is not None:
+        r.set_tile_owners(owner)
     if accum is not None:
         r.write_accum(accum)
     r.set_loop_num(loop_num)

@@ -113,8 +113,9 @@ def test_empty_scene_renders_the_environment(gpu_renderer, env_maps):
         assert bit_mismatch(img, ref)[0] == 0.0
 
 
+@pytest.mark.parametrize("assign", ["modulo", "balanced"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
+def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world, assign):
     """Ranks r = 0..world-1 render their interleaved tiles (one context each, as one process per
     GPU would); the rank-major concatenation of their device tile buffers, un-permuted by
     rt_assemble_frame on the device, is the single-rank frame bit for bit (and the oracle's)."""
@@ -125,11 +126,23 @@ def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
     fp = cf.frame_params(W, H)
     ro, frames = frames_for(fp, 1, 2)
     ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    owner = None
+    if assign == "balanced":  # bench.py's cost-balanced owner map (rt_tile_costs + tiling.balance)
+        r0 = gpu_renderer
+        r0.set_scene_soa(sd.soa, sd.nodes)
+        r0.set_env(*env_maps)
+        r0.resize(W, H, tile=T)
+        before = r0.read_accum()
+        costs = r0.tile_costs(fp, ro[:1])
+        assert np.array_equal(costs, r0.tile_costs(fp, ro[:1])) and costs.min() > 0
+        assert r0.loop_num == 0 and np.array_equal(r0.read_accum(), before)  # the probe leaves no trace
+        owner = tiling.balance(costs, world)
+        assert not np.array_equal(owner, tiling.modulo_owners(W, H, T, T, world))
     parts = []
     ctxs = [gpu_renderer] + [Renderer(0) for _ in range(world - 1)]
     try:
         for rank, r in enumerate(ctxs):
-            gpu_render(r, sd, env_maps, W, H, fp, ro, tile=T, rank=rank, world=world)
+            gpu_render(r, sd, env_maps, W, H, fp, ro, tile=T, rank=rank, world=world, owner=owner)
             info = r.accum_device()
             buf = torch.empty(info["bytes"] // 4, dtype=torch.float32, device="cuda")
             torch.cuda.synchronize()  # buf allocated on torch's stream, copied on the ctx stream
@@ -142,8 +155,8 @@ def test_tile_split_and_device_assembly(gpu_renderer, env_maps, world):
         ctxs[0].assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
         torch.cuda.synchronize()
         img = frame.cpu().numpy().reshape(H, W, 3)
-        mlt = tiling.max_local_tiles(W, H, T, T, world)
-        host = tiling.assemble(gathered.cpu().numpy().reshape(world, mlt, T, T, 4), W, H, T, T, world)
+        mlt = tiling.max_local_tiles(W, H, T, T, world, owner)
+        host = tiling.assemble(gathered.cpu().numpy().reshape(world, mlt, T, T, 4), W, H, T, T, world, owner)
     finally:
         for r in ctxs[1:]:
             r.close()

@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
-"""Per-rank scaling estimate on one GPU: rank 0's tile share of an N-rank run (bench.py's
-tiling and path budget), timed alone for N = 1, 2, 4, 8.  Strong-scaling efficiency of the
-render part = t(1) / (N * t(N)) (the frame-end gather is not included)."""
+"""Per-rank balance of the N-rank bench on one GPU: EVERY rank's tile share of an N-rank run
+(bench.py's tiling, frames per step and path budget) rendered alone, for N = 1, 2, 4, 8.
+
+The bench's value at N ranks is rays of all ranks / the slowest rank's time, so the render part's
+strong-scaling efficiency is t(1) / (N * max_r t_r(N)); the imbalance max/mean says how much of
+the loss is the tile assignment (the frame-end gather is not included).  Prints one JSON line
+per N and, with --out, writes them all to a file.
+
+    python tools/rank_sim.py [--frames 1024] [--reps 1] [--worlds 1,2,4,8]
+"""
 import argparse
+import json
 import sys
 import time
 from pathlib import Path
@@ -10,36 +18,61 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "opengl-ray-tracing-framework_amd"))
 from rtamd import configs as cf  # noqa: E402
+from rtamd import tiling  # noqa: E402
 from rtamd.renderer import Renderer  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--frames", type=int, default=512)
-ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--config", default="C3")
+ap.add_argument("--frames", type=int, default=1024)
+ap.add_argument("--reps", type=int, default=1)
 ap.add_argument("--worlds", default="1,2,4,8")
+ap.add_argument("--tile", type=int, default=32)
+ap.add_argument("--out", default=None)
+ap.add_argument("--assign", default="both", choices=["modulo", "balanced", "both"],
+                help="tile owner map: interleaved t %% N, bench.py's cost-balanced map, or both")
 a = ap.parse_args()
-sd = cf.config_scene("C3")
+cfg = cf.CONFIGS[a.config]
+sd = cf.config_scene(a.config)
 env = cf.load_env()
-W, H = 1920, 1080
+W, H = cfg.width, cfg.height
 fp = cf.frame_params(W, H)
-ro = cf.rand_origins(a.frames)
+ro = cf.rand_origins(a.frames + 1)
+r = Renderer(0)
+r.set_scene_soa(sd.soa, sd.nodes)
+r.set_env(*env)
+lines = []
+# full-frame tile costs (what bench.py's ranks assemble from their shares with an all_reduce)
+r.resize(W, H, tile=a.tile)
+costs = r.tile_costs(fp, ro[-1:])
 t1 = None
-for world in [int(x) for x in a.worlds.split(",")]:
-    r = Renderer(0)
-    r.set_scene_soa(sd.soa, sd.nodes)
-    r.set_env(*env)
-    r.resize(W, H, tile=32, rank=0, world=world)
-    ad = r.accum_device()
-    r.set_max_paths(a.frames * ad["local_tiles"] * 32 * 32)
-    r.render(fp, ro)
-    r.reset_stats()
-    r.synchronize()
-    t = time.perf_counter()
-    for _ in range(a.reps):
-        r.render_async(fp, ro)
-    r.synchronize()
-    dt = (time.perf_counter() - t) / a.reps
-    st = r.stats()
-    t1 = dt if t1 is None else t1
-    print(f"world {world}: rank-0 step {dt * 1e3:.1f} ms, {st['rays'] / a.reps / dt / 1e6:.0f} Mrays/s per rank, "
-          f"efficiency vs N=1 {t1 / (world * dt):.3f}", flush=True)
-    r.close()
+modes = ["modulo", "balanced"] if a.assign == "both" else [a.assign]
+for world, mode in [(int(x), m) for x in a.worlds.split(",") for m in modes]:
+    if world == 1 and mode == "balanced":
+        continue
+    owner = tiling.balance(costs, world) if mode == "balanced" else None
+    times, rays = [], []
+    for rank in range(world):
+        r.resize(W, H, tile=a.tile, rank=rank, world=world)
+        if owner is not None:
+            r.set_tile_owners(owner)
+        ad = r.accum_device()
+        r.set_max_paths(a.frames * ad["local_tiles"] * a.tile * a.tile)
+        r.render(fp, ro[1:a.frames + 1])          # warm: path-state allocation, first launches
+        r.synchronize()
+        r.reset_stats()
+        t = time.perf_counter()
+        for _ in range(a.reps):
+            r.render_async(fp, ro[1:a.frames + 1])
+        r.synchronize()
+        times.append((time.perf_counter() - t) / a.reps)
+        rays.append(r.stats()["rays"] / a.reps)
+    tmax, tmean = max(times), sum(times) / len(times)
+    t1 = tmax if t1 is None else t1
+    d = {"config": a.config, "world": world, "assign": mode, "frames": a.frames, "rank_ms": [round(x * 1e3, 1) for x in times],
+         "max_ms": round(tmax * 1e3, 1), "mean_ms": round(tmean * 1e3, 1), "imbalance": round(tmax / tmean, 4),
+         "mrays_per_s_job": round(sum(rays) / tmax / 1e6, 1), "efficiency_vs_n1": round(t1 / (world * tmax), 4)}
+    lines.append(d)
+    print(json.dumps(d), flush=True)
+r.close()
+if a.out:
+    Path(a.out).write_text("\n".join(json.dumps(x) for x in lines) + "\n")
