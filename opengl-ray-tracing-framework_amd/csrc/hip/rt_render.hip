@@ -14,6 +14,7 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <limits>
 
 #include "rt_abi.h"
 #include "rt_kernels.h"
@@ -454,6 +455,29 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     return idx;
   };
   qroot = is_leaf(croot) ? croot : build(croot, 1);
+  const char* qb = getenv("RT_QBFS");
+  if (!is_leaf(qroot) && !(qb && atoi(qb) == 0)) {
+    // breadth-first numbering (RT_QBFS=0: depth-first): the top levels of the tree are the
+    // first nodes (RT_DEBUG_PASSES reports node visits by this index)
+    std::vector<int> order{qroot}, newid(qn.size(), -1);
+    newid[qroot] = 0;
+    for (size_t h = 0; h < order.size(); h++) {
+      const int4 r = qn[order[h]].ref;
+      for (int x : {r.x, r.y, r.z, r.w})
+        if (x != rtd::Q_EMPTY && !is_leaf(x)) {
+          newid[x] = (int)order.size();
+          order.push_back(x);
+        }
+    }
+    std::vector<rtd::QNode> bq(order.size());
+    auto remap = [&](int x) { return (x == rtd::Q_EMPTY || is_leaf(x)) ? x : newid[x]; };
+    for (size_t i = 0; i < order.size(); i++) {
+      bq[i] = qn[order[i]];
+      bq[i].ref = make_int4(remap(bq[i].ref.x), remap(bq[i].ref.y), remap(bq[i].ref.z), remap(bq[i].ref.w));
+    }
+    qn.swap(bq);
+    qroot = 0;
+  }
   return true;
 }
 
@@ -1163,8 +1187,13 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       HIPCHK(c, hipGetLastError());
       c->trace_launches++;
     } else {
-      // split the batch into frame groups (frames [f0, f1) each), one stream per group
-      const int G = std::min(c->n_groups, nf);
+      // split the batch into frame groups (frames [f0, f1) each), one stream per group; a batch
+      // of fewer frames than groups (one frame per call: the reference's own usage) is split by
+      // pixels instead (work items [w0, w1) each, all frames), so the groups' latency-bound late
+      // passes still overlap each other
+      static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
+      const bool pix_split = pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
+      const int G = pix_split ? c->n_groups : std::min(c->n_groups, nf);
       static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
       const unsigned int trace_grid = (unsigned)(c->n_cus * std::max(c->trace_bpc, c->trace_bpc0));
       const unsigned int trace_grid0 = (unsigned)(c->n_cus * c->trace_bpc0);
@@ -1180,32 +1209,39 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       hipStream_t sg[rt_ctx::MAX_GROUPS];
       unsigned int slots_g[rt_ctx::MAX_GROUPS];
       for (int g = 0; g < G; g++) {
-        const int f0 = g * nf / G, f1 = (g + 1) * nf / G;
+        const int f0 = pix_split ? 0 : g * nf / G, f1 = pix_split ? nf : (g + 1) * nf / G;
+        const unsigned int w0 = pix_split ? (unsigned)((size_t)c->n_valid * g / G) : 0u;
+        const unsigned int w1 = pix_split ? (unsigned)((size_t)c->n_valid * (g + 1) / G) : (unsigned)c->n_valid;
         rtd::WFParams& WP = WG[g];
         WP.K = P;
         WP.K.loop_num = P.loop_num + f0;
         WP.K.rand_origin = P.rand_origin + f0;
         WP.K.sobol = P.sobol + 4 * f0;
         WP.K.n_frames = f1 - f0;
-        WP.K.n_work = (unsigned)c->n_valid;
+        WP.K.n_work = w1 - w0;
         WP.K.lds_entries = c->trace_lds_entries;
         WP.K.pool_chunk = c->pool_chunk;
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)g * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
         WP.K.wave_log = (debug_passes && count) ? d_wave_log : nullptr;
         WP.S = c->wfg[g];
-        WP.S.pix_xy = c->wf.pix_xy;
-        WP.S.pix_acc = c->wf.pix_acc;
-        WP.S.cam = c->wf.cam;
+        WP.S.pix_xy = c->wf.pix_xy + w0;
+        WP.S.pix_acc = c->wf.pix_acc + w0;
+        WP.S.cam = c->wf.cam + w0;
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
-        slots_g[g] = (unsigned)(f1 - f0) * (unsigned)c->n_valid;
+        slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
         sg[g] = g == 0 ? c->stream : c->aux[g];
       }
-      // camera directions of this call's frames (every group reads them)
+      // camera directions of this call's pixels (every group reads them)
+      rtd::WFParams WC = WG[0];
+      WC.K.n_work = (unsigned)c->n_valid;
+      WC.S.pix_xy = c->wf.pix_xy;
+      WC.S.pix_acc = c->wf.pix_acc;
+      WC.S.cam = c->wf.cam;
       hipLaunchKernelGGL(rtd::wf_camera, dim3(std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256))),
-                         dim3(256), 0, c->stream, WG[0]);
+                         dim3(256), 0, c->stream, WC);
       HIPCHK(c, hipGetLastError());
       // aux streams start after everything already queued on the caller's stream
       if (G > 1) {
@@ -1222,7 +1258,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       hipEvent_t prev_stagger = nullptr, prev_blend = nullptr;
       for (int g = 0; g < G; g++) {
         rtd::WFParams& WP = WG[g];
-        if (prev_stagger) {
+        if (prev_stagger) {  // (pixel groups start together: nothing to wait for)
           HIPCHK(c, hipStreamWaitEvent(sg[g], prev_stagger, 0));
           c->event_pool.push_back(prev_stagger);  // reusable once the wait is enqueued
         }
@@ -1260,6 +1296,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
             fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
                     "wave-iters max %llu ray-steps max %llu\n", g, pass, (WP.cam_n ? WP.cam_n : q[0]), ms, h[2], h[3], h[4], h[5], h[6], h[7]);
+            unsigned long long hq[6];
+            HIPCHK(c, hipMemcpy(hq, c->d_stats + 22, sizeof(hq), hipMemcpyDeviceToHost));
+            fprintf(stderr, "[rt]   4-wide node visits with BFS index < 1 / 5 / 21 / 64 / 85 / 341: %llu %llu %llu %llu %llu %llu\n",
+                    hq[0], hq[1], hq[2], hq[3], hq[4], hq[5]);
+            HIPCHK(c, hipMemset(c->d_stats + 22, 0, sizeof(hq)));
             fprintf(stderr, "[rt]   lane utilisation: node phase %.3f (%llu iters)  tri phase %.3f (%llu iters)  busy at "
                     "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
                     h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
@@ -1294,29 +1335,32 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           else
             hipLaunchKernelGGL(rtd::wf_shade<false>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
           HIPCHK(c, hipGetLastError());
-          if (g + 1 < G && pass == std::min(c->stagger, last_pass)) {
+          if (!pix_split && g + 1 < G && pass == std::min(c->stagger, last_pass)) {
             prev_stagger = take_event(c);
             if (!prev_stagger) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
             HIPCHK(c, hipEventRecord(prev_stagger, sg[g]));
           }
         }
-        // progressive blend in frame order: group g after group g-1
+        // progressive blend in frame order: group g after group g-1 (pixel groups blend
+        // disjoint pixels: no order between them)
         if (prev_blend) {
           HIPCHK(c, hipStreamWaitEvent(sg[g], prev_blend, 0));
           c->event_pool.push_back(prev_blend);
         }
         hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WP);
         HIPCHK(c, hipGetLastError());
-        if (g + 1 < G) {
+        if (!pix_split && g + 1 < G) {
           prev_blend = take_event(c);
           if (!prev_blend) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(prev_blend, sg[g]));
         }
       }
-      if (G > 1) {  // the caller's stream joins the last group
+      // the caller's stream joins the last group (frame groups finish in order through their
+      // blends) or every group (pixel groups)
+      for (int g = pix_split ? 1 : G - 1; g < G && G > 1; g++) {
         hipEvent_t ej = take_event(c);
         if (!ej) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
-        HIPCHK(c, hipEventRecord(ej, sg[G - 1]));
+        HIPCHK(c, hipEventRecord(ej, sg[g]));
         HIPCHK(c, hipStreamWaitEvent(c->stream, ej, 0));
         c->event_pool.push_back(ej);
       }

@@ -560,6 +560,7 @@ void wf_trace(const WFParams W) {
   unsigned int ray_steps = 0, ray_steps_max = 0;  // COUNT: node + triangle steps of the lane's ray
   unsigned long long v_itN = 0, v_itT = 0, v_itO = 0, v_park = 0, v_busyO = 0;  // COUNT: lane utilisation
   unsigned long long v_rays = 0;
+  unsigned long long v_q[6] = {0, 0, 0, 0, 0, 0};  // COUNT: node visits by breadth-first index
   const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
   const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
 
@@ -649,7 +650,13 @@ void wf_trace(const WFParams W) {
               L.haveCur = tl_pop(P, L, TS, cull);
             }
           } else {
-            if (COUNT) { v_int++; ray_steps++; }
+            if (COUNT) {
+              v_int++; ray_steps++;
+              if (WIDE) {  // node-visit histogram by breadth-first index (the LDS cache candidates)
+                v_q[0] += L.cur < 1; v_q[1] += L.cur < 5; v_q[2] += L.cur < 21;
+                v_q[3] += L.cur < 64; v_q[4] += L.cur < 85; v_q[5] += L.cur < 341;
+              }
+            }
             if (WIDE) tl_qnode(P, L, TS, cull);
             else tl_node(P, L, TS, cull);
           }
@@ -754,6 +761,11 @@ void wf_trace(const WFParams W) {
       v_tri += __shfl_xor(v_tri, off);
       v_park += __shfl_xor(v_park, off);
       v_busyO += __shfl_xor(v_busyO, off);
+    }
+    for (int q = 0; q < 6; q++) {
+      unsigned long long x = v_q[q];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+      if ((threadIdx.x & 63) == 0 && x) atomicAdd(&P.stats[22 + q], x);
     }
     if ((threadIdx.x & 63) == 0) {  // wave-uniform iteration counts + lane-sums
       atomicAdd(&P.stats[8], v_itN);

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc_cmp.sh: per variant and kernel, the summed durations and counters, VALU
+issue fraction (4 cycles per wave64 VALU instruction on a 16-lane SIMD, 1024 SIMDs), lane
+utilisation, L2 hit rate."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+
+def kname(r):
+    return r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].replace("rtd::", "")
+
+
+root, variants = sys.argv[1], sys.argv[2:]
+for v in variants:
+    dur = defaultdict(float)
+    for f in glob.glob(f"{root}/{v}/t/**/run_kernel_trace.csv", recursive=True) + glob.glob(f"{root}/{v}/t/run_kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            dur[kname(r)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    cnt = defaultdict(lambda: defaultdict(float))
+    for p in ("a", "b"):
+        for f in set(glob.glob(f"{root}/{v}/{p}/**/run_counter_collection.csv", recursive=True) +
+                     glob.glob(f"{root}/{v}/{p}/run_counter_collection.csv")):
+            for r in csv.DictReader(open(f)):
+                cnt[kname(r)][r["Counter_Name"]] += float(r["Counter_Value"])
+    print(f"== {v}")
+    for k in sorted(dur, key=lambda k: -dur[k]):
+        if not k.startswith("wf_") and "rt_" not in k:
+            continue
+        c = cnt.get(k, {})
+        line = f"  {k:12s} {dur[k]:9.2f} ms"
+        if c.get("SQ_INSTS_VALU"):
+            cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8
+            line += f"  valu {c['SQ_INSTS_VALU']:.3e}"
+            if cyc:
+                line += f"  issue {c['SQ_INSTS_VALU'] * 4 / (1024 * cyc):.3f}  clk {cyc / (dur[k] * 1e6):.2f}GHz"
+            if c.get("SQ_ACTIVE_INST_VALU"):
+                line += f"  lanes {c['SQ_THREAD_CYCLES_VALU'] / (64 * c['SQ_ACTIVE_INST_VALU']):.3f}"
+            if c.get("SQ_WAVE_CYCLES"):
+                line += f"  wait {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.2f}"
+            line += f"  vmem {c.get('SQ_INSTS_VMEM_RD', 0):.3e}  salu {c.get('SQ_INSTS_SALU', 0):.3e}"
+        if c.get("TCC_HIT_sum"):
+            line += f"  L2hit {c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']):.3f}"
+        print(line)
