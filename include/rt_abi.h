@@ -97,7 +97,9 @@ typedef struct rt_frame_params {
 enum {
   RT_FLAG_NO_CULL = 1,            /* disable closest-hit box culling (exhaustive RT:338 order)  */
   RT_FLAG_COUNT_VISITS = 2,       /* also count node/triangle visits (slower)                  */
-  RT_FLAG_MEGAKERNEL = 4          /* single persistent megakernel instead of the wavefront path */
+  RT_FLAG_MEGAKERNEL = 4,         /* single persistent megakernel instead of the wavefront path */
+  RT_FLAG_NO_FINISH = 8,          /* never end paths in the path-persistent finisher            */
+  RT_FLAG_FINISH = 16             /* use the finisher whatever the batch size (rt_set_finish)   */
 };
 
 typedef struct rt_stats {
@@ -149,6 +151,12 @@ int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_
  * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL
  * counterpart: the fragment shader has one path per pixel in flight. */
 int rt_set_max_paths(rt_ctx* ctx, uint64_t slots);
+/* Path-persistent finisher (no GL counterpart: main.cpp:175-200 draws one frame per loop pass,
+ * and each wavefront pass of such a small batch waits for its slowest ray).  A frame group of at
+ * most max_slots path slots runs passes 0 .. pass-1 as wavefront passes and then ends every path
+ * in one launch, one lane per path (results unchanged).  pass 0 disables it; defaults 2 and 8 Mi
+ * slots (1080p: up to 8 frames per group).  RT_FLAG_NO_FINISH / RT_FLAG_FINISH override per call. */
+int rt_set_finish(rt_ctx* ctx, int32_t pass, uint64_t max_slots);
 
 /* Enqueue n_frames progressive frames (one randOrigin per frame) on the ctx stream.  Each
  * frame first applies main.cpp:175 (LoopNum++ unless it reached max_iterations). */

@@ -103,6 +103,11 @@ struct rt_ctx {
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
   size_t max_slots_req = 0;        // rt_set_max_paths (0: RT_MAX_SLOTS or the 320 Mi default)
+  // path-persistent finisher (wf_finish): a frame group of at most finish_slots path slots runs
+  // passes 0 .. finish_pass-1 as wavefront passes, then one wf_finish launch ends every path
+  int finish_pass = 2;  // C3 1080p single frames: 1 / 2 / 3 -> 3.73 / 3.35 / 3.41 ms (off: 3.79)
+  uint64_t finish_slots = uint64_t(8) << 20;
+  int finish_bpc = 0;              // wf_finish blocks per CU
 };
 
 namespace {
@@ -554,6 +559,14 @@ int occupancy(rt_ctx* c) {
       fprintf(stderr, "[rt]   occupancy(lds=%d) = %d\n", l, b);
     }
   }
+  {
+    int b = 0;
+    const hipError_t e = c->wide
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_finish<true, true>, 256, c->trace_lds)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_finish<true, false>, 256, c->trace_lds);
+    // the finisher's lanes index the traversal overflow column: never more than the trace grid
+    c->finish_bpc = std::max(1, std::min(e == hipSuccess ? b : 1, std::max(c->trace_bpc, c->trace_bpc0)));
+  }
   const size_t lanes = (size_t)c->n_cus * std::max(c->trace_bpc, c->trace_bpc0) * 256;
   const int entries = std::max(c->stack_entries, c->qstack_entries);
   const size_t need = (size_t)std::max(0, entries - kl) * lanes * sizeof(int2) * c->n_groups;
@@ -566,8 +579,15 @@ int occupancy(rt_ctx* c) {
 }
 
 template <bool COUNT, bool WIDE>
-void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
+void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
   const int mode = WP.pass == 0 ? c->trace_mode0 : c->trace_mode;
+  if (small && !COUNT && WIDE && mode == rtd::TM_DUAL) {  // static first shares of mid-size passes
+    if (WP.cam_n)
+      hipLaunchKernelGGL((rtd::wf_trace<false, rtd::TM_DUAL, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
+    else
+      hipLaunchKernelGGL((rtd::wf_trace<false, rtd::TM_DUAL, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
+    return;
+  }
 #define RT_LAUNCH_TRACE(M)                                                                                  \
   if (WP.cam_n)                                                                                           \
     hipLaunchKernelGGL((rtd::wf_trace<COUNT, M, WIDE, true>), grid, dim3(256), c->trace_lds, st, WP);      \
@@ -583,14 +603,15 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
 }
 
 template <bool COUNT>
-void launch_trace_t(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
-  if (c->wide) launch_trace_w<COUNT, true>(c, grid, WP, st);
-  else launch_trace_w<COUNT, false>(c, grid, WP, st);
+void launch_trace_t(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
+  if (c->wide) launch_trace_w<COUNT, true>(c, grid, WP, st, small);
+  else launch_trace_w<COUNT, false>(c, grid, WP, st, small);
 }
 
-void launch_trace(rt_ctx* c, bool count, dim3 grid, const rtd::WFParams& WP, hipStream_t st) {
-  if (count) launch_trace_t<true>(c, grid, WP, st);
-  else launch_trace_t<false>(c, grid, WP, st);
+// small: a frame group of at most finish_slots path slots (one frame per call)
+void launch_trace(rt_ctx* c, bool count, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
+  if (count) launch_trace_t<true>(c, grid, WP, st, small);
+  else launch_trace_t<false>(c, grid, WP, st, small);
 }
 
 hipEvent_t take_event(rt_ctx* c) {
@@ -694,8 +715,10 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
   if (const char* e = getenv("RT_STAGES")) c->stages = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
-  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 32 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)) != hipSuccess) {
+  if (const char* e = getenv("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
+  if (const char* e = getenv("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
+  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -1071,6 +1094,13 @@ int rt_get_loop_num(const rt_ctx* c, int32_t* n) {
   *n = c->loop_num;
   return RT_OK;
 }
+int rt_set_finish(rt_ctx* c, int32_t pass, uint64_t max_slots) {
+  if (!c || pass < 0) return RT_ERR_ARG;
+  c->finish_pass = pass;
+  c->finish_slots = max_slots;
+  return RT_OK;
+}
+
 int rt_clear_accum(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
@@ -1267,8 +1297,24 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         // the group's frames start in `stages` steps, one per pass (see wf_gen)
         const int nfg = WP.n_frames;
         const int stages = std::max(1, std::min(c->stages, nfg));
+        // small groups (one frame per call) end their paths in wf_finish after pass finish_pass-1
+        const bool finish = stages == 1 && !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
+                            c->finish_pass >= 1 && c->finish_pass <= last_pass &&
+                            ((fp->flags & RT_FLAG_FINISH) || slots_g[g] <= c->finish_slots);
         for (int pass = 0; pass <= last_pass + stages - 1; pass++) {
           WP.pass = pass;
+          if (finish && pass == c->finish_pass) {
+            const dim3 fgrid((unsigned)(c->n_cus * c->finish_bpc));
+            if (fp->enable_bsdf) {
+              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+              else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+            } else {
+              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<false, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+              else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+            }
+            HIPCHK(c, hipGetLastError());
+            break;
+          }
           // one stage: pass 0's camera paths are implicit (wf_trace / wf_shade generate them)
           WP.cam_n = (stages == 1 && pass == 0) ? slots_g[g] : 0u;
           if (pass < stages && stages > 1) {
@@ -1281,7 +1327,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));
-          launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g]);
+          launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g], slots_g[g] <= c->finish_slots);
           HIPCHK(c, hipGetLastError());
           HIPCHK(c, hipEventRecord(t1, sg[g]));
           c->trace_events.push_back({t0, t1});
@@ -1305,6 +1351,17 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
                     "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
                     h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
             HIPCHK(c, hipMemset(c->d_stats + 6, 0, 10 * sizeof(unsigned long long)));
+            {  // steps-per-ray histogram (16-step buckets) by ray kind
+              unsigned long long hh[64];
+              HIPCHK(c, hipMemcpy(hh, c->d_stats + 32, sizeof(hh), hipMemcpyDeviceToHost));
+              static const char* kinds[4] = {"cont miss", "cont hit ", "shad miss", "shad hit "};
+              for (int kd = 0; kd < 4; kd++) {
+                fprintf(stderr, "[rt]   steps/ray %s:", kinds[kd]);
+                for (int b = 0; b < 16; b++) fprintf(stderr, " %llu", hh[kd * 16 + b]);
+                fprintf(stderr, "\n");
+              }
+              HIPCHK(c, hipMemset(c->d_stats + 32, 0, sizeof(hh)));
+            }
             if (WP.K.wave_log) {
               HIPCHK(c, hipMemcpy(wave_log.data(), d_wave_log, wave_log.size() * 8, hipMemcpyDeviceToHost));
               unsigned long long t0min = ~0ull, t1max = 0, t0max = 0, dmax = 0, itmax = 0, rmax = 0, cmax = 0;
@@ -1424,7 +1481,7 @@ int rt_stats_reset(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)));
+  HIPCHK(c, hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)));
   c->kernel_ms = 0.0;
   c->launches = 0;
   c->trace_ms = 0.0;

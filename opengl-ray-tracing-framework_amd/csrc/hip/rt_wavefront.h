@@ -487,6 +487,52 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   L.haveCur = r[0] != Q_EMPTY || tl_pop(P, L, S, cull);
 }
 
+// start a ray on a lane whose origin, direction and anyhit are set: 1/d, plane offsets, root
+template <bool WIDE>
+RTD void tl_start(const KParams& P, TraceLane& L) {
+  L.ix = 1.0f / L.dx; L.iy = 1.0f / L.dy; L.iz = 1.0f / L.dz;
+  // finite 1/d: per axis (lo-o)*inv <= (hi-o)*inv exactly when inv > 0 (rounding is
+  // monotone), so the slab min/max of RT:309-310 is a fixed choice of plane per ray
+  L.finite = fabs_(L.ix) < INFINITY && fabs_(L.iy) < INFINITY && fabs_(L.iz) < INFINITY;
+  L.offNx = L.ix > 0.0f ? 0 : 48;
+  L.offNy = L.iy > 0.0f ? 16 : 64;
+  L.offNz = L.iz > 0.0f ? 32 : 80;
+  L.best = INF;
+  L.besttri = -1;
+  L.bestt = 0.0f;
+  L.sp = 0;
+  L.cur = WIDE ? P.qroot : P.root;
+  L.haveCur = true;
+  L.tri_i = L.tri_end = 0;
+}
+
+// one dual-cursor step of a lane's ray (see TM_DUAL): one triangle of the current leaf and one
+// node; true when the ray is finished (stack empty and leaf done, or an any-hit found)
+template <bool WIDE>
+RTD bool tl_dual_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull) {
+  bool finished = false;
+  if (L.tri_i < L.tri_end) {
+    if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+      finished = true;
+      L.tri_end = L.tri_i;
+    }
+  }
+  if (!finished && L.haveCur) {
+    if (ref_is_leaf(L.cur)) {
+      if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
+        L.tri_i = leaf_first(L.cur);
+        L.tri_end = L.tri_i + leaf_count(L.cur);
+        L.haveCur = tl_pop(P, L, TS, cull);
+      }
+    } else if (WIDE) {
+      tl_qnode(P, L, TS, cull);
+    } else {
+      tl_node(P, L, TS, cull);
+    }
+  }
+  return finished || (!L.haveCur && L.tri_i >= L.tri_end);
+}
+
 #ifndef RT_TRACE_WPE
 #define RT_TRACE_WPE 1
 #endif
@@ -504,12 +550,16 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
 #endif
+#ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed)
+#define RT_STATIC_FRAC 4
+#endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
 #endif
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
-// passes' kernels carry none of its registers
-template <bool COUNT, int MODE, bool WIDE, bool CAM>
+// passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
+// a separate instantiation: the code alone cost the bulk's kernels 0.4%)
+template <bool COUNT, int MODE, bool WIDE, bool CAM, bool STATIC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == TM_DUAL ? RT_TRACE_WPE_DUAL : RT_TRACE_WPE)))
 void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -547,7 +597,20 @@ void wf_trace(const WFParams W) {
   // only as many waves as the queue can feed take part: every claim is an atomic on one word,
   // and thousands of empty-handed claims in a small late pass serialise at that address
   const unsigned int wave_id = blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6);
-  bool drained = wave_id >= (nq + RT_TAIL_CHUNK - 1u) / RT_TAIL_CHUNK;
+  const unsigned int part_waves = min(gridDim.x * (TL_LANES / 64), (nq + RT_TAIL_CHUNK - 1u) / RT_TAIL_CHUNK);
+  bool drained = wave_id >= part_waves;
+  // a pass smaller than the tail threshold would be claimed entirely in 64-ray chunks, and a
+  // single counter serves only ~90 claims/us (a 1080p frame's first passes: 16 K - 28 K claims);
+  // so in small groups (STATIC: one frame per call) each participating wave first takes
+  // a static share of RT_STATIC_FRAC/8 of the queue and only the rest is claimed dynamically
+  // (C3 1080p single frames: 3.97 -> 3.68 ms; the bulk's late passes lost 0.4% with it)
+  const unsigned int static_per = (STATIC && RT_STATIC_FRAC > 0 && nq <= tail_rays)
+      ? (unsigned int)((unsigned long long)nq * RT_STATIC_FRAC / 8u / part_waves) : 0u;
+  const unsigned int static_total = static_per * part_waves;
+  if (STATIC && !drained) {
+    pool_next = wave_id * static_per;
+    pool_end = pool_next + static_per;
+  }
   const int lane = (int)(threadIdx.x & 63);
   int entry = 0, parked = 0;
   bool haveParked = false;
@@ -579,7 +642,7 @@ void wf_trace(const WFParams W) {
         const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+        base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= nq) {
           drained = true;
         } else {
@@ -608,20 +671,7 @@ void wf_trace(const WFParams W) {
             L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
             L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
           }
-          L.ix = 1.0f / L.dx; L.iy = 1.0f / L.dy; L.iz = 1.0f / L.dz;
-          // finite 1/d: per axis (lo-o)*inv <= (hi-o)*inv exactly when inv > 0 (rounding is
-          // monotone), so the slab min/max of RT:309-310 is a fixed choice of plane per ray
-          L.finite = fabs_(L.ix) < INFINITY && fabs_(L.iy) < INFINITY && fabs_(L.iz) < INFINITY;
-          L.offNx = L.ix > 0.0f ? 0 : 48;
-          L.offNy = L.iy > 0.0f ? 16 : 64;
-          L.offNz = L.iz > 0.0f ? 32 : 80;
-          L.best = INF;
-          L.besttri = -1;
-          L.bestt = 0.0f;
-          L.sp = 0;
-          L.cur = WIDE ? P.qroot : P.root;
-          L.haveCur = true;
-          L.tri_i = L.tri_end = 0;
+          tl_start<WIDE>(P, L);
           haveParked = false;
           busy = true;
         }
@@ -741,6 +791,8 @@ void wf_trace(const WFParams W) {
           atomicAdd(&P.tile_cost[S.pix_acc[w] / (unsigned int)(P.tile_w * P.tile_h)],
                     (unsigned long long)(ray_steps + RT_COST_PER_RAY));
         }
+        if (P.wave_log)  // RT_DEBUG_PASSES: steps-per-ray histogram by kind (16-step buckets)
+          atomicAdd(&P.stats[32 + (L.anyhit ? 32 : 0) + (L.besttri >= 0 ? 16 : 0) + min(15u, ray_steps / 16u)], 1ull);
         ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; v_rays++;
       }
       busy = false;
@@ -836,6 +888,330 @@ constexpr int SH_SUB = RT_SH_SUB;
 #define SHP_MARK(i)
 #endif
 
+// One path's shade step (the body of wf_shade, shared with wf_finish): consume the traced results
+// of the current bounce, sample the next one, write the state back and return the rays to queue.
+// camPass: the implicit camera pass (state built from the slot); loadPrev: the path has state
+// from an earlier pass (every pass but 0).
+struct ShadeOut {
+  bool qShadow, qCont;
+};
+template <bool BSDF>
+RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
+                        unsigned long long& nsamples) {
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  bool doFinish = false, doBounce = false;
+  bool qShadow = false, qCont = false;
+  f3 fin = splat(0.0f);
+  float4 a0 = make_float4(0, 0, 0, 0), a1 = a0, a2 = a0, a3 = a0, a4 = a0;
+  uint4 a5 = make_uint4(0, 0, 0, 0);
+  f3 hist = splat(1.0f), Lo = splat(0.0f), Le0 = splat(0.0f), evf = splat(0.0f);
+  float evp = 0.0f;
+  uint32_t wseed = 0, bounce = 0, flags = 0, frame = 0;
+  f3 hP = splat(0.0f), hN = splat(0.0f), hV = splat(0.0f);
+  float hDist = 0.0f;
+  int mat = 0;
+  if (live) {
+    float4 cam_d = make_float4(0, 0, 0, 0);
+    if (camPass) {  // implicit camera pass: the state wf_gen would have written
+      uint32_t cseed, cframe;
+      const f3 d = camera_ray(P, S, (unsigned)path, cseed, cframe);
+      a5 = make_uint4(cseed, 0u, PF_CONT | PF_CAMERA, cframe);
+      cam_d = make_float4(d.x, d.y, d.z, 0.0f);
+    } else {
+#if RT_S5_PACK
+      const uint2 p5 = S.s5[path];
+      const unsigned int nfr = (unsigned int)W.n_frames;
+      a5 = make_uint4(p5.x, p5.y >> 8, p5.y & 0xffu, (unsigned int)path % nfr);
+#else
+      a5 = S.s5[path];
+#endif
+    }
+    // every load of the path's state issues at once: camera paths exist only in pass 0 (a
+    // uniform test), so no load waits for the flags; the flags still decide what is used
+    int2 rsh = make_int2(0, 0);
+    if (loadPrev) {
+      a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path]; a3 = S.s3[path];
+      rsh = S.res[2 * path + 1];
+    }
+    const int2 rc0 = S.res[2 * path];
+    const float4 oo0 = camPass ? make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f) : S.ro[path];
+    const float4 dd0 = camPass ? cam_d : S.rd[path];
+    wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
+    if (!(flags & PF_CAMERA)) {
+      hist = xyz(a0); evp = a0.w;
+      Lo = xyz(a1);
+      evf = xyz(a2);
+      Le0 = mk3(a1.w, a2.w, 0.0f);
+      Le0.z = a3.w;
+      // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
+      if ((flags & PF_SHADOW) && rsh.x < 0) Lo = Lo + xyz(a3);
+      // ---- pending medium-emissive term (RT:1437-1439)
+      if (flags & PF_CMED) {
+        a4 = S.s4[path];
+        Lo = Lo + xyz(a4);
+      }
+    }
+    if (!(flags & PF_CONT)) {  // BSDF pdf was 0 (RT:1460-1462): the path ends
+      fin = Le0 + Lo;
+      doFinish = true;
+    } else {
+      const int2 r = rc0;
+      const float4 oo = oo0, dd = dd0;
+      const f3 ro = xyz(oo), rd = xyz(dd);
+      if (r.x >= 0) {
+        const int tri = r.x;
+        const float t = __int_as_float(r.y);
+        const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
+        const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
+        const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+        const f3 ng = mk3(A.w, B.w, Cc.w);
+        const bool inside = dot(ng, rd) > 0.0f;
+        const f3 Pp = ro + rd * t;
+        const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
+                            (-(p1.x - p2.x) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
+        const float beta = (-(Pp.x - p3.x) * (p1.y - p3.y) + (Pp.y - p3.y) * (p1.x - p3.x)) /
+                           (-(p2.x - p3.x) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
+        const float gama = 1.0f - alpha - beta;
+        const f3 Ns = normalize(alpha * xyz(N1) + beta * xyz(N2) + gama * xyz(N3));
+        const int nmat = __float_as_int(N1.w);
+        if (flags & PF_CAMERA) {  // RT:1541-1544
+          Le0 = xyz(P.mats[8 * nmat]);
+          Lo = splat(0.0f);
+          hist = splat(1.0f);
+          bounce = 0;
+        } else if (BSDF) {  // RT:1509-1510
+          const f3 Le = xyz(P.mats[8 * nmat]);
+          Lo = Lo + hist * Le * evf / evp;
+          bounce++;
+        } else {  // BRDF mode RT:1362-1364 (evf = f_r, evp = pdf_brdf, s4.x = N.L)
+          const f3 Le = xyz(P.mats[8 * nmat]);
+          Lo = Lo + hist * Le * evf * fabs_(S.s4[path].x) / evp;
+          bounce++;
+        }
+        hP = Pp;
+        hN = inside ? -Ns : Ns;
+        hV = rd;
+        hDist = t - 0.00001f;
+        mat = nmat;
+        if ((int)bounce < P.max_bounce) doBounce = true;
+        else { fin = Le0 + Lo; doFinish = true; }
+      } else if (flags & PF_CAMERA) {  // RT:1532-1539
+        fin = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
+        doFinish = true;
+      } else if (!BSDF) {  // BRDF mode RT:1345-1359
+        const float aNdotL = fabs_(S.s4[path].x);
+        if (P.enable_env) {
+          f3 skyColor;
+          float pdf_light;
+          hdrColorPdf(E, rd, skyColor, pdf_light);
+          skyColor = skyColor * E.intensity;
+          const float mis_weight = misMixWeight(evp, pdf_light);
+          Lo = Lo + mis_weight * hist * skyColor * evf * aNdotL / evp;
+        } else {
+          const f3 skyColor = getDefaultSkyColor(rd.y);
+          Lo = Lo + hist * skyColor * evf * aNdotL / evp;
+        }
+        fin = Le0 + Lo;
+        doFinish = true;
+      } else {  // RT:1483-1506
+        if (P.enable_env) {
+          f3 light_fr;
+          float light_pdf;
+          hdrColorPdf(E, rd, light_fr, light_pdf);
+          light_fr = light_fr * E.intensity;
+          float mis_weight = misMixWeight(evp, light_pdf);
+          if (!P.enable_mis) mis_weight = 1.0f;
+          if (!(flags & PF_MEDIUM)) Lo = Lo + mis_weight * hist * light_fr * evf / evp;
+          else Lo = Lo + hist * light_fr * evf / light_pdf;
+        } else {
+          const f3 light_fr = getDefaultSkyColor(rd.y);
+          Lo = Lo + hist * light_fr * evf / evp;
+        }
+        fin = Le0 + Lo;
+        doFinish = true;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------- next bounce
+  f3 cnee = splat(0.0f), cmed = splat(0.0f);
+  uint32_t nflags = 0;
+  f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
+  float bNdotL = 0.0f;  // BRDF mode: N.L of the sampled direction (RT:1336)
+  if (doBounce && !BSDF) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
+    const Mat m = load_mat(P.mats, mat);
+    const f3 V = -hV, N = hN;
+    const float xa = rand_(wseed);
+    const float xb = rand_(wseed);
+    const f3 Ll = SampleHdr(E, xa, xb);
+    f3 T, Bt;
+    getTangent(N, T, Bt);
+    if (dot(N, Ll) > 0.0f) {
+      f3 light_fr;
+      float light_pdf;
+      hdrColorPdf(E, Ll, light_fr, light_pdf);
+      light_fr = light_fr * E.intensity;
+      float brdf_pdf;
+      const f3 brdf_fr = BRDF_Evaluate(V, N, Ll, T, Bt, m, brdf_pdf);
+      const float mis_weight = misMixWeight(light_pdf, brdf_pdf);
+      cnee = mis_weight * hist * light_fr * brdf_fr * fabs_(dot(N, Ll)) / light_pdf;
+      shO = hP;
+      shD = Ll;
+      qShadow = true;
+      nflags |= PF_SHADOW;
+    }
+    float sx, sy;
+#if RT_SOBOL_TABLE
+    sobol_pair(P, frame, bounce, sx, sy);
+#else
+    int g = P.loop_num[frame] + 1;
+    g = g ^ (g >> 1);
+    sx = sobol_gray((int)bounce * 2, g);
+    sy = sobol_gray((int)bounce * 2 + 1, g);
+#endif
+    const float cu = rand_(wseed), cv = rand_(wseed);
+    sx += cu;
+    if (sx > 1) sx -= 1;
+    if (sx < 0) sx += 1;
+    sy += cv;
+    if (sy > 1) sy -= 1;
+    if (sy < 0) sy += 1;
+    const float xi_3 = rand_(wseed);
+    const f3 L = SampleBRDF(sx, sy, xi_3, V, N, m);
+    bNdotL = dot(N, L);
+    float pdf_brdf;
+    const f3 f_r = BRDF_Evaluate(V, N, L, T, Bt, m, pdf_brdf);
+    if (pdf_brdf > 0.0f) {
+      hist = hist * (f_r * fabs_(bNdotL) / pdf_brdf);
+      evf = f_r;
+      evp = pdf_brdf;
+      contO = hP;
+      contD = L;
+      qCont = true;
+      nflags |= PF_CONT;
+    }
+    if (!qShadow && !qCont) {
+      fin = Le0 + Lo;
+      doFinish = true;
+    }
+  } else if (doBounce) {
+    const Mat m = load_mat(P.mats, mat);
+    const f3 V = -hV;
+    const BsdfFrame BF = bsdf_frame(m, V, hN);  // shared by the three BSDF calls below
+    // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
+    const float xa = rand_(wseed);  // R24
+    const float xb = rand_(wseed);
+    const f3 Ll = SampleHdr(E, xa, xb);
+    if (dot(hN, Ll) > 0.0f) {
+      f3 light_fr;
+      float light_pdf;
+      hdrColorPdf(E, Ll, light_fr, light_pdf);
+      light_fr = light_fr * E.intensity;
+      float disney_eval_pdf;
+      const f3 disney_eval_fr = DisneyEval(BF, m, hN, Ll, disney_eval_pdf);
+      float mis_weight = misMixWeight(light_pdf, disney_eval_pdf);
+      if (!P.enable_mis) mis_weight = 1.0f;
+      cnee = mis_weight * hist * light_fr * disney_eval_fr / light_pdf;
+      shO = hP;
+      shD = Ll;
+      qShadow = true;
+      nflags |= PF_SHADOW;
+    }
+    // BSDF sample (RT:1408-1474)
+    float sx, sy;
+#if RT_SOBOL_TABLE
+    sobol_pair(P, frame, bounce, sx, sy);
+#else
+    int g = P.loop_num[frame] + 1;
+    g = g ^ (g >> 1);
+    sx = sobol_gray((int)bounce * 2, g);
+    sy = sobol_gray((int)bounce * 2 + 1, g);
+#endif
+    const float cu = rand_(wseed), cv = rand_(wseed);
+    sx += cu;
+    if (sx > 1) sx -= 1;
+    if (sx < 0) sx += 1;
+    sy += cv;
+    if (sy > 1) sy -= 1;
+    if (sy < 0) sy += 1;
+    const float xi_3 = rand_(wseed);
+    f3 L;
+    float pdf;
+    bool isRefract;
+    const f3 fr = DisneySample(BF, sx, sy, xi_3, m, hN, L, pdf, isRefract);
+    bool medS = false;
+    float scatter_pdf = 0.0f;
+    float transmittance = 1.0f;
+    if (pdf > 0.0f) {
+      if (!isRefract) {
+        hist = hist * (fr / pdf);
+      } else if (m.mtype == MEDIUM_ABSORB) {
+        hist = hist * exp3(-(splat(1.0f) - m.mcolor) * hDist * m.mdensity);
+      } else if (m.mtype == MEDIUM_EMISSIVE) {
+        cmed = m.mcolor * hDist * m.mdensity * hist;
+        nflags |= PF_CMED;
+      } else if (m.mtype == MEDIUM_SCATTER) {
+        const float scatterDist = min_(-log_(xi_3) / m.mdensity, hDist);
+        medS = scatterDist < hDist;
+        if (medS) {
+          transmittance *= exp_(-1.0f * scatterDist);
+          hist = hist * (m.mcolor * transmittance);
+          hP = hP + hV * scatterDist;
+          const f3 scatterDir = SampleHG(V, m.manis, sx, sy);
+          scatter_pdf = PhaseHG(dot(V, scatterDir), m.manis);
+          L = scatterDir;
+        }
+      }
+      evf = DisneyEval(BF, m, hN, L, evp);
+      if (medS && scatter_pdf > 0.0f) {
+        evp = scatter_pdf;
+        evf = splat(scatter_pdf);
+      }
+      if (medS) nflags |= PF_MEDIUM;
+      contO = hP;
+      contD = L;
+      qCont = true;
+      nflags |= PF_CONT;
+    }
+    if (!qShadow && !qCont) {  // no ray left: finish now (RT:1460-1462 break)
+      fin = Le0 + Lo;
+      doFinish = true;
+    }
+  }
+
+  // ----------------------------------------------------------- progressive blend
+  if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
+    S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
+    nsamples++;
+  }
+
+  // ------------------------------------------------------------ enqueue rays
+  const bool keep = qShadow || qCont;
+  if (keep) {
+    S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
+    S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
+    S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
+    S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
+    if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
+    if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
+#if RT_S5_PACK
+    S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
+#else
+    S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
+#endif
+    if (qCont) {
+      S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
+      S.rd[path] = make_float4(contD.x, contD.y, contD.z, 0.0f);
+    }
+    if (qShadow) {
+      S.so[path] = make_float4(shO.x, shO.y, shO.z, 0.0f);
+      S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
+    }
+  }
+  return ShadeOut{qShadow, qCont};
+}
+
 // BSDF: enableBSDF (RT:1369 Disney integrator) or the BRDF integrator (RT:1290), one
 // instantiation each so neither carries the other's registers
 template <bool BSDF>
@@ -908,327 +1284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
-    bool doFinish = false, doBounce = false;
-    bool qShadow = false, qCont = false;
-    f3 fin = splat(0.0f);
-    float4 a0 = make_float4(0, 0, 0, 0), a1 = a0, a2 = a0, a3 = a0, a4 = a0;
-    uint4 a5 = make_uint4(0, 0, 0, 0);
-    f3 hist = splat(1.0f), Lo = splat(0.0f), Le0 = splat(0.0f), evf = splat(0.0f);
-    float evp = 0.0f;
-    uint32_t wseed = 0, bounce = 0, flags = 0, frame = 0;
-    f3 hP = splat(0.0f), hN = splat(0.0f), hV = splat(0.0f);
-    float hDist = 0.0f;
-    int mat = 0;
-    if (live) {
-      float4 cam_d = make_float4(0, 0, 0, 0);
-      if (W.cam_n) {  // implicit camera pass: the state wf_gen would have written
-        uint32_t cseed, cframe;
-        const f3 d = camera_ray(P, S, (unsigned)path, cseed, cframe);
-        a5 = make_uint4(cseed, 0u, PF_CONT | PF_CAMERA, cframe);
-        cam_d = make_float4(d.x, d.y, d.z, 0.0f);
-      } else {
-#if RT_S5_PACK
-        const uint2 p5 = S.s5[path];
-        const unsigned int nfr = (unsigned int)W.n_frames;
-        a5 = make_uint4(p5.x, p5.y >> 8, p5.y & 0xffu, (unsigned int)path % nfr);
-#else
-        a5 = S.s5[path];
-#endif
-      }
-      // every load of the path's state issues at once: camera paths exist only in pass 0 (a
-      // uniform test), so no load waits for the flags; the flags still decide what is used
-      int2 rsh = make_int2(0, 0);
-      if (W.pass != 0) {
-        a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path]; a3 = S.s3[path];
-        rsh = S.res[2 * path + 1];
-      }
-      const int2 rc0 = S.res[2 * path];
-      const float4 oo0 = W.cam_n ? make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f) : S.ro[path];
-      const float4 dd0 = W.cam_n ? cam_d : S.rd[path];
-      wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
-      if (!(flags & PF_CAMERA)) {
-        hist = xyz(a0); evp = a0.w;
-        Lo = xyz(a1);
-        evf = xyz(a2);
-        Le0 = mk3(a1.w, a2.w, 0.0f);
-        Le0.z = a3.w;
-        // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
-        if ((flags & PF_SHADOW) && rsh.x < 0) Lo = Lo + xyz(a3);
-        // ---- pending medium-emissive term (RT:1437-1439)
-        if (flags & PF_CMED) {
-          a4 = S.s4[path];
-          Lo = Lo + xyz(a4);
-        }
-      }
-      if (!(flags & PF_CONT)) {  // BSDF pdf was 0 (RT:1460-1462): the path ends
-        fin = Le0 + Lo;
-        doFinish = true;
-      } else {
-        const int2 r = rc0;
-        const float4 oo = oo0, dd = dd0;
-        const f3 ro = xyz(oo), rd = xyz(dd);
-        if (r.x >= 0) {
-          const int tri = r.x;
-          const float t = __int_as_float(r.y);
-          const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
-          const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
-          const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
-          const f3 ng = mk3(A.w, B.w, Cc.w);
-          const bool inside = dot(ng, rd) > 0.0f;
-          const f3 Pp = ro + rd * t;
-          const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
-                              (-(p1.x - p2.x) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
-          const float beta = (-(Pp.x - p3.x) * (p1.y - p3.y) + (Pp.y - p3.y) * (p1.x - p3.x)) /
-                             (-(p2.x - p3.x) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
-          const float gama = 1.0f - alpha - beta;
-          const f3 Ns = normalize(alpha * xyz(N1) + beta * xyz(N2) + gama * xyz(N3));
-          const int nmat = __float_as_int(N1.w);
-          if (flags & PF_CAMERA) {  // RT:1541-1544
-            Le0 = xyz(P.mats[8 * nmat]);
-            Lo = splat(0.0f);
-            hist = splat(1.0f);
-            bounce = 0;
-          } else if (BSDF) {  // RT:1509-1510
-            const f3 Le = xyz(P.mats[8 * nmat]);
-            Lo = Lo + hist * Le * evf / evp;
-            bounce++;
-          } else {  // BRDF mode RT:1362-1364 (evf = f_r, evp = pdf_brdf, s4.x = N.L)
-            const f3 Le = xyz(P.mats[8 * nmat]);
-            Lo = Lo + hist * Le * evf * fabs_(S.s4[path].x) / evp;
-            bounce++;
-          }
-          hP = Pp;
-          hN = inside ? -Ns : Ns;
-          hV = rd;
-          hDist = t - 0.00001f;
-          mat = nmat;
-          if ((int)bounce < P.max_bounce) doBounce = true;
-          else { fin = Le0 + Lo; doFinish = true; }
-        } else if (flags & PF_CAMERA) {  // RT:1532-1539
-          fin = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
-          doFinish = true;
-        } else if (!BSDF) {  // BRDF mode RT:1345-1359
-          const float aNdotL = fabs_(S.s4[path].x);
-          if (P.enable_env) {
-            f3 skyColor;
-            float pdf_light;
-            hdrColorPdf(E, rd, skyColor, pdf_light);
-            skyColor = skyColor * E.intensity;
-            const float mis_weight = misMixWeight(evp, pdf_light);
-            Lo = Lo + mis_weight * hist * skyColor * evf * aNdotL / evp;
-          } else {
-            const f3 skyColor = getDefaultSkyColor(rd.y);
-            Lo = Lo + hist * skyColor * evf * aNdotL / evp;
-          }
-          fin = Le0 + Lo;
-          doFinish = true;
-        } else {  // RT:1483-1506
-          if (P.enable_env) {
-            f3 light_fr;
-            float light_pdf;
-            hdrColorPdf(E, rd, light_fr, light_pdf);
-            light_fr = light_fr * E.intensity;
-            float mis_weight = misMixWeight(evp, light_pdf);
-            if (!P.enable_mis) mis_weight = 1.0f;
-            if (!(flags & PF_MEDIUM)) Lo = Lo + mis_weight * hist * light_fr * evf / evp;
-            else Lo = Lo + hist * light_fr * evf / light_pdf;
-          } else {
-            const f3 light_fr = getDefaultSkyColor(rd.y);
-            Lo = Lo + hist * light_fr * evf / evp;
-          }
-          fin = Le0 + Lo;
-          doFinish = true;
-        }
-      }
-    }
-
-    SHP_MARK(1)
-#ifdef RT_SHADE_PROF
-    unsigned long long shp_mid = 0;
-#endif
-    // ------------------------------------------------------------- next bounce
-    f3 cnee = splat(0.0f), cmed = splat(0.0f);
-    uint32_t nflags = 0;
-    f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
-    float bNdotL = 0.0f;  // BRDF mode: N.L of the sampled direction (RT:1336)
-    if (doBounce && !BSDF) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
-      const Mat m = load_mat(P.mats, mat);
-      const f3 V = -hV, N = hN;
-      const float xa = rand_(wseed);
-      const float xb = rand_(wseed);
-      const f3 Ll = SampleHdr(E, xa, xb);
-      f3 T, Bt;
-      getTangent(N, T, Bt);
-      if (dot(N, Ll) > 0.0f) {
-        f3 light_fr;
-        float light_pdf;
-        hdrColorPdf(E, Ll, light_fr, light_pdf);
-        light_fr = light_fr * E.intensity;
-        float brdf_pdf;
-        const f3 brdf_fr = BRDF_Evaluate(V, N, Ll, T, Bt, m, brdf_pdf);
-        const float mis_weight = misMixWeight(light_pdf, brdf_pdf);
-        cnee = mis_weight * hist * light_fr * brdf_fr * fabs_(dot(N, Ll)) / light_pdf;
-        shO = hP;
-        shD = Ll;
-        qShadow = true;
-        nflags |= PF_SHADOW;
-      }
-      float sx, sy;
-#if RT_SOBOL_TABLE
-      sobol_pair(P, frame, bounce, sx, sy);
-#else
-      int g = P.loop_num[frame] + 1;
-      g = g ^ (g >> 1);
-      sx = sobol_gray((int)bounce * 2, g);
-      sy = sobol_gray((int)bounce * 2 + 1, g);
-#endif
-      const float cu = rand_(wseed), cv = rand_(wseed);
-      sx += cu;
-      if (sx > 1) sx -= 1;
-      if (sx < 0) sx += 1;
-      sy += cv;
-      if (sy > 1) sy -= 1;
-      if (sy < 0) sy += 1;
-      const float xi_3 = rand_(wseed);
-      const f3 L = SampleBRDF(sx, sy, xi_3, V, N, m);
-      bNdotL = dot(N, L);
-      float pdf_brdf;
-      const f3 f_r = BRDF_Evaluate(V, N, L, T, Bt, m, pdf_brdf);
-      if (pdf_brdf > 0.0f) {
-        hist = hist * (f_r * fabs_(bNdotL) / pdf_brdf);
-        evf = f_r;
-        evp = pdf_brdf;
-        contO = hP;
-        contD = L;
-        qCont = true;
-        nflags |= PF_CONT;
-      }
-      if (!qShadow && !qCont) {
-        fin = Le0 + Lo;
-        doFinish = true;
-      }
-    } else if (doBounce) {
-      const Mat m = load_mat(P.mats, mat);
-      const f3 V = -hV;
-      const BsdfFrame BF = bsdf_frame(m, V, hN);  // shared by the three BSDF calls below
-      // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
-      const float xa = rand_(wseed);  // R24
-      const float xb = rand_(wseed);
-      const f3 Ll = SampleHdr(E, xa, xb);
-      if (dot(hN, Ll) > 0.0f) {
-        f3 light_fr;
-        float light_pdf;
-        hdrColorPdf(E, Ll, light_fr, light_pdf);
-        light_fr = light_fr * E.intensity;
-        float disney_eval_pdf;
-        const f3 disney_eval_fr = DisneyEval(BF, m, hN, Ll, disney_eval_pdf);
-        float mis_weight = misMixWeight(light_pdf, disney_eval_pdf);
-        if (!P.enable_mis) mis_weight = 1.0f;
-        cnee = mis_weight * hist * light_fr * disney_eval_fr / light_pdf;
-        shO = hP;
-        shD = Ll;
-        qShadow = true;
-        nflags |= PF_SHADOW;
-      }
-#ifdef RT_SHADE_PROF
-      shp_mid = clock64();
-#endif
-      // BSDF sample (RT:1408-1474)
-      float sx, sy;
-#if RT_SOBOL_TABLE
-      sobol_pair(P, frame, bounce, sx, sy);
-#else
-      int g = P.loop_num[frame] + 1;
-      g = g ^ (g >> 1);
-      sx = sobol_gray((int)bounce * 2, g);
-      sy = sobol_gray((int)bounce * 2 + 1, g);
-#endif
-      const float cu = rand_(wseed), cv = rand_(wseed);
-      sx += cu;
-      if (sx > 1) sx -= 1;
-      if (sx < 0) sx += 1;
-      sy += cv;
-      if (sy > 1) sy -= 1;
-      if (sy < 0) sy += 1;
-      const float xi_3 = rand_(wseed);
-      f3 L;
-      float pdf;
-      bool isRefract;
-      const f3 fr = DisneySample(BF, sx, sy, xi_3, m, hN, L, pdf, isRefract);
-      bool medS = false;
-      float scatter_pdf = 0.0f;
-      float transmittance = 1.0f;
-      if (pdf > 0.0f) {
-        if (!isRefract) {
-          hist = hist * (fr / pdf);
-        } else if (m.mtype == MEDIUM_ABSORB) {
-          hist = hist * exp3(-(splat(1.0f) - m.mcolor) * hDist * m.mdensity);
-        } else if (m.mtype == MEDIUM_EMISSIVE) {
-          cmed = m.mcolor * hDist * m.mdensity * hist;
-          nflags |= PF_CMED;
-        } else if (m.mtype == MEDIUM_SCATTER) {
-          const float scatterDist = min_(-log_(xi_3) / m.mdensity, hDist);
-          medS = scatterDist < hDist;
-          if (medS) {
-            transmittance *= exp_(-1.0f * scatterDist);
-            hist = hist * (m.mcolor * transmittance);
-            hP = hP + hV * scatterDist;
-            const f3 scatterDir = SampleHG(V, m.manis, sx, sy);
-            scatter_pdf = PhaseHG(dot(V, scatterDir), m.manis);
-            L = scatterDir;
-          }
-        }
-        evf = DisneyEval(BF, m, hN, L, evp);
-        if (medS && scatter_pdf > 0.0f) {
-          evp = scatter_pdf;
-          evf = splat(scatter_pdf);
-        }
-        if (medS) nflags |= PF_MEDIUM;
-        contO = hP;
-        contD = L;
-        qCont = true;
-        nflags |= PF_CONT;
-      }
-      if (!qShadow && !qCont) {  // no ray left: finish now (RT:1460-1462 break)
-        fin = Le0 + Lo;
-        doFinish = true;
-      }
-    }
-
-#ifdef RT_SHADE_PROF
-    for (int off = 32; off > 0; off >>= 1) shp_mid = max(shp_mid, (unsigned long long)__shfl_xor((long long)shp_mid, off));
-    if (shp_mid > shp_t) { shp[2] += shp_mid - shp_t; shp_t = shp_mid; }
-    SHP_MARK(3)
-#endif
-    // ----------------------------------------------------------- progressive blend
-    if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
-      S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
-      nsamples++;
-    }
-
-    // ------------------------------------------------------------ enqueue rays
-    const bool keep = qShadow || qCont;
-    if (keep) {
-      S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
-      S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
-      S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
-      S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
-      if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
-      if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
-#if RT_S5_PACK
-      S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
-#else
-      S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
-#endif
-      if (qCont) {
-        S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
-        S.rd[path] = make_float4(contD.x, contD.y, contD.z, 0.0f);
-      }
-      if (qShadow) {
-        S.so[path] = make_float4(shO.x, shO.y, shO.z, 0.0f);
-        S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
-      }
-    }
+    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
+    const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
     const unsigned int qs = wave_lds_append(&lc[0], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u));
     if (qShadow) lq[qs] = (path << 1) | 1;
     if (qCont) lq[qs + (qShadow ? 1u : 0u)] = path << 1;
@@ -1257,6 +1314,115 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     nsamples += __shfl_xor(nsamples, off);
   }
   if ((threadIdx.x & 63) == 0 && (nrays | nsamples)) {
+    atomicAdd(&P.stats[0], nrays);
+    atomicAdd(&P.stats[1], nsamples);
+  }
+}
+
+// ---------------------------------------------------------------------------- finish
+// Path-persistent finisher for small batches (one frame per render call: the reference's own
+// usage, main.cpp:175-200).  Every wavefront pass waits for its slowest ray (150-250 traversal
+// steps at ~1 us each, whatever the pass size), so the late passes of a single 1080p frame cost
+// ~0.2 ms each while tracing only thousands of rays.  After pass F-1's shade, wf_finish gives each
+// remaining path one lane, which traces the path's queued rays (shadow, then continuation: the
+// same dual-cursor step as wf_trace) and runs the path's shade step (shade_path, as wf_shade),
+// bounce after bounce until the path ends; a lane whose path ended takes the next one from the
+// active list.  A wave's chain is then its longest remaining path instead of the sum over passes
+// of each pass's longest ray.  Same device functions in the same order per path: the image and
+// the ray count are unchanged.
+#ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
+#define RT_FINISH_SHADE_MIN 16
+#endif
+#ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
+#define RT_FINISH_WPE 2
+#endif
+template <bool BSDF, bool WIDE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FINISH_WPE)))
+void wf_finish(const WFParams W) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const int in = W.pass & 1;
+  const unsigned int na = S.cnt[2 + in];
+  const int lane = (int)(threadIdx.x & 63);
+  // only as many waves as the list can feed take part (one lane per path)
+  if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
+  const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+  TraceStack TS;
+  TS.KL = P.lds_entries;
+  TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
+  TS.ovf = (gu64*)(P.stack_ovf) + (blockIdx.x * TL_LANES + threadIdx.x);
+  TS.ovs = P.ovf_lanes;
+  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
+  unsigned long long nrays = 0, nsamples = 0;
+  // lane state: no path / tracing the path's queued rays / rays done, waiting for its shade step
+  enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
+  int st = FS_IDLE, path = 0;
+  bool drained = false, contNext = false;
+  TraceLane L;
+  L.anyhit = false;
+  // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation
+  auto begin_rays = [&](bool sh, bool co) {
+    contNext = sh && co;
+    L.anyhit = sh;
+    const float4 oo = sh ? S.so[path] : S.ro[path];
+    const float4 dd = sh ? S.sd[path] : S.rd[path];
+    L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
+    L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+    tl_start<WIDE>(P, L);
+  };
+  while (true) {
+    // idle lanes take the next paths of the active list (one atomic per wave)
+    const unsigned long long idle = __ballot(st == FS_IDLE);
+    if (idle && !drained) {
+      const unsigned int want = (unsigned int)__popcll(idle);
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(&S.cnt[4], want);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+      const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
+      if (st == FS_IDLE && idx < na) {
+        path = S.active[in][idx];
+#if RT_S5_PACK
+        const uint32_t flags = S.s5[path].y & 0xffu;
+#else
+        const uint32_t flags = S.s5[path].z;
+#endif
+        st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
+        begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
+      }
+      drained = base + want >= na;
+    }
+    if (!__any(st != FS_IDLE)) break;
+    // trace until enough lanes wait for their shade step (or none is tracing): a lane never waits
+    // for the wave's slowest ray of every bounce, only for a batch of shade steps
+    while (true) {
+      const unsigned long long tr = __ballot(st == FS_TRACE);
+      if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
+      if (st == FS_TRACE && (!P.has_scene || tl_dual_step<WIDE>(P, L, TS, cull))) {
+        S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
+        nrays++;
+        if (contNext) begin_rays(false, true);
+        else st = FS_SHADE;
+      }
+    }
+    if (__any(st == FS_SHADE)) {
+      const bool sh = st == FS_SHADE;
+      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
+      if (sh) {
+        if (o.qShadow || o.qCont) {
+          st = FS_TRACE;
+          begin_rays(o.qShadow, o.qCont);
+        } else {
+          st = FS_IDLE;
+        }
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    nrays += __shfl_xor(nrays, off);
+    nsamples += __shfl_xor(nsamples, off);
+  }
+  if (lane == 0) {
     atomicAdd(&P.stats[0], nrays);
     atomicAdd(&P.stats[1], nsamples);
   }

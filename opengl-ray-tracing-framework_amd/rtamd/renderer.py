@@ -22,6 +22,8 @@ RT_MAX_FRAMES_PER_LAUNCH = 1024
 RT_FLAG_NO_CULL = 1
 RT_FLAG_COUNT_VISITS = 2
 RT_FLAG_MEGAKERNEL = 4
+RT_FLAG_NO_FINISH = 8
+RT_FLAG_FINISH = 16
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 
 _f32p = C.POINTER(C.c_float)
@@ -34,7 +36,7 @@ ABI_SYMBOLS = (
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
-    "rt_tile_costs",
+    "rt_tile_costs", "rt_set_finish",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -175,6 +177,8 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_assemble_frame.argtypes = [vp, vp, C.c_int32, vp]
     L.rt_tonemap.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_uint8)]
     L.rt_set_max_paths.argtypes = [vp, C.c_uint64]
+    if hasattr(L, "rt_set_finish"):  # (absent from older builds loaded for A/B timing)
+        L.rt_set_finish.argtypes = [vp, C.c_int32, C.c_uint64]
     L.rt_set_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
@@ -314,6 +318,11 @@ class Renderer:
     def set_max_paths(self, slots: int) -> None:
         """Path-state budget in pixel-frames (0: the library default); see rt_abi.h."""
         self._check(self._L.rt_set_max_paths(self._h, int(slots)), "rt_set_max_paths")
+
+    def set_finish(self, pass_: int, max_slots: int) -> None:
+        """rt_set_finish: end paths in the path-persistent finisher after pass `pass_ - 1` for frame
+        groups of at most `max_slots` path slots (pass_ 0: never)."""
+        self._check(self._L.rt_set_finish(self._h, int(pass_), int(max_slots)), "rt_set_finish")
 
     def clear_accum(self) -> None:
         self._check(self._L.rt_clear_accum(self._h), "rt_clear_accum")

@@ -150,3 +150,28 @@ def test_bsdf_mode_env_and_mis_switches(gpu_renderer, env_maps, env, mis):
     ref, _ = oracle_render(sd, env_maps, W, H, frames)
     img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("bsdf", [1, 0], ids=["bsdf", "brdf"])
+@pytest.mark.parametrize("finish", ["off", "pass1", "pass2", "pass8"])
+@pytest.mark.parametrize("name", ["C3", "C4"])
+def test_path_persistent_finisher_matches_oracle(gpu_renderer, env_maps, name, finish, bsdf):
+    """wf_finish (one lane per remaining path, trace + shade until the path ends) against the
+    pure pass-by-pass wavefront and the oracle, for every pass it can take over from: the image
+    bits and the ray count are unchanged.  C4's glass keeps paths alive through refraction."""
+    from rtamd.renderer import RT_FLAG_FINISH, RT_FLAG_NO_FINISH
+    sd = cf.config_scene(name)
+    W, H = 80, 48
+    flags = RT_FLAG_NO_FINISH if finish == "off" else RT_FLAG_FINISH
+    fp = cf.frame_params(W, H, flags=flags)
+    fp.enable_bsdf = bsdf
+    ro, frames = frames_for(fp, 1, 2)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    if finish != "off":
+        gpu_renderer.set_finish(int(finish[4:]), 1 << 30)
+    try:
+        img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    finally:
+        gpu_renderer.set_finish(2, 8 << 20)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
