@@ -1350,6 +1350,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             fprintf(stderr, "[rt]   lane utilisation: node phase %.3f (%llu iters)  tri phase %.3f (%llu iters)  busy at "
                     "refill %.3f (%llu outer)\n", h[9] / (64.0 * (double)(h[8] + !h[8])), h[8],
                     h[11] / (64.0 * (double)(h[10] + !h[10])), h[10], h[13] / (64.0 * (double)(h[12] + !h[12])), h[12]);
+            fprintf(stderr, "[rt]   overflow-column pushes %llu (%.3f per ray)\n", h[14],
+                    (double)h[14] / (double)std::max(1u, WP.cam_n ? WP.cam_n : q[0]));
             HIPCHK(c, hipMemset(c->d_stats + 6, 0, 10 * sizeof(unsigned long long)));
             {  // steps-per-ray histogram (16-step buckets) by ray kind
               unsigned long long hh[64];

@@ -622,7 +622,7 @@ void wf_trace(const WFParams W) {
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;
   unsigned int ray_steps = 0, ray_steps_max = 0;  // COUNT: node + triangle steps of the lane's ray
   unsigned long long v_itN = 0, v_itT = 0, v_itO = 0, v_park = 0, v_busyO = 0;  // COUNT: lane utilisation
-  unsigned long long v_rays = 0;
+  unsigned long long v_rays = 0, v_ovf = 0;  // COUNT: rays, overflow-column pushes
   unsigned long long v_q[6] = {0, 0, 0, 0, 0, 0};  // COUNT: node visits by breadth-first index
   const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
   const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
@@ -707,8 +707,10 @@ void wf_trace(const WFParams W) {
                 v_q[3] += L.cur < 64; v_q[4] += L.cur < 85; v_q[5] += L.cur < 341;
               }
             }
+            const int sp0 = L.sp;
             if (WIDE) tl_qnode(P, L, TS, cull);
             else tl_node(P, L, TS, cull);
+            if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
           }
         }
         if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
@@ -813,6 +815,7 @@ void wf_trace(const WFParams W) {
       v_tri += __shfl_xor(v_tri, off);
       v_park += __shfl_xor(v_park, off);
       v_busyO += __shfl_xor(v_busyO, off);
+      v_ovf += __shfl_xor(v_ovf, off);
     }
     for (int q = 0; q < 6; q++) {
       unsigned long long x = v_q[q];
@@ -826,6 +829,7 @@ void wf_trace(const WFParams W) {
       atomicAdd(&P.stats[11], v_tri);
       atomicAdd(&P.stats[12], v_itO);
       atomicAdd(&P.stats[13], v_busyO);
+      atomicAdd(&P.stats[14], v_ovf);
     }
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&P.stats[2], v_int);
