@@ -1305,6 +1305,13 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           WP.pass = pass;
           if (finish && pass == c->finish_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * c->finish_bpc));
+            static const bool fin_prof = getenv("RT_FINISH_PROF") != nullptr;  // development (RT_FINISH_PROF builds)
+            static unsigned long long* d_fin_log = nullptr;                    // never freed
+            if (fin_prof) {
+              if (!d_fin_log) HIPCHK(c, hipMalloc(&d_fin_log, (size_t)fgrid.x * 4 * 8 * 8));
+              HIPCHK(c, hipMemsetAsync(d_fin_log, 0, (size_t)fgrid.x * 4 * 8 * 8, sg[g]));
+              WP.K.wave_log = d_fin_log;
+            }
             if (fp->enable_bsdf) {
               if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
               else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
@@ -1313,6 +1320,27 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
             }
             HIPCHK(c, hipGetLastError());
+            if (fin_prof) {  // per-wave summary of this launch (syncs)
+              std::vector<unsigned long long> lg((size_t)fgrid.x * 4 * 8);
+              HIPCHK(c, hipStreamSynchronize(sg[g]));
+              HIPCHK(c, hipMemcpy(lg.data(), d_fin_log, lg.size() * 8, hipMemcpyDeviceToHost));
+              WP.K.wave_log = nullptr;
+              unsigned long long t0 = ~0ull;
+              std::vector<size_t> ws;
+              for (size_t i = 0; i < lg.size() / 8; i++)
+                if (lg[8 * i + 1]) { t0 = std::min(t0, lg[8 * i]); ws.push_back(i); }
+              std::sort(ws.begin(), ws.end(), [&](size_t a, size_t b) { return lg[8 * a + 1] > lg[8 * b + 1]; });
+              fprintf(stderr, "[rt] wf_finish group %d: %zu working waves\n", g, ws.size());
+              for (size_t k = 0; k < ws.size() && k < 6; k++) {
+                const unsigned long long* e = &lg[8 * ws[k]];
+                fprintf(stderr, "[rt]   wave end %.1f us (start %.1f): trace iters %llu, shade steps %llu, rays %llu, paths %llu, "
+                        "longest ray %llu iters\n", (e[1] - t0) / 100.0, (e[0] - t0) / 100.0, e[2], e[3], e[4], e[5],
+                        e[7]);
+              }
+              if (!ws.empty())
+                fprintf(stderr, "[rt]   wave ends: 50%% %.1f us, 90%% %.1f, 99%% %.1f\n", (lg[8 * ws[ws.size() / 2] + 1] - t0) / 100.0,
+                        (lg[8 * ws[ws.size() / 10] + 1] - t0) / 100.0, (lg[8 * ws[ws.size() / 100] + 1] - t0) / 100.0);
+            }
             break;
           }
           // one stage: pass 0's camera paths are implicit (wf_trace / wf_shade generate them)

@@ -1365,8 +1365,17 @@ void wf_finish(const WFParams W) {
   bool drained = false, contNext = false;
   TraceLane L;
   L.anyhit = false;
+#ifdef RT_FINISH_PROF  // development: per-wave timeline of the finisher -> P.wave_log (RT_FINISH_PROF env)
+  unsigned long long fp_it = 0, fp_sh = 0, fp_paths = 0;
+  unsigned int fp_ray = 0, fp_raymax = 0;
+  const unsigned long long fp_t0 = wall_clock64();
+#define FPROF(x) x
+#else
+#define FPROF(x)
+#endif
   // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation
   auto begin_rays = [&](bool sh, bool co) {
+    FPROF(fp_raymax = max(fp_raymax, fp_ray); fp_ray = 0;)
     contNext = sh && co;
     L.anyhit = sh;
     const float4 oo = sh ? S.so[path] : S.ro[path];
@@ -1393,6 +1402,7 @@ void wf_finish(const WFParams W) {
 #endif
         st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
         begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
+        FPROF(fp_paths++;)
       }
       drained = base + want >= na;
     }
@@ -1402,6 +1412,7 @@ void wf_finish(const WFParams W) {
     while (true) {
       const unsigned long long tr = __ballot(st == FS_TRACE);
       if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
+      FPROF(fp_it++; if (st == FS_TRACE) fp_ray++;)
       if (st == FS_TRACE && (!P.has_scene || tl_dual_step<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
         nrays++;
@@ -1410,6 +1421,7 @@ void wf_finish(const WFParams W) {
       }
     }
     if (__any(st == FS_SHADE)) {
+      FPROF(fp_sh++;)
       const bool sh = st == FS_SHADE;
       const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
       if (sh) {
@@ -1430,6 +1442,19 @@ void wf_finish(const WFParams W) {
     atomicAdd(&P.stats[0], nrays);
     atomicAdd(&P.stats[1], nsamples);
   }
+#ifdef RT_FINISH_PROF
+  fp_raymax = max(fp_raymax, fp_ray);
+  for (int off = 32; off > 0; off >>= 1) {
+    fp_paths += __shfl_xor(fp_paths, off);
+    fp_raymax = max(fp_raymax, (unsigned)__shfl_xor((int)fp_raymax, off));
+  }
+  if (P.wave_log && lane == 0) {
+    unsigned long long* o = P.wave_log + 8 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+    o[0] = fp_t0; o[1] = wall_clock64(); o[2] = fp_it; o[3] = fp_sh; o[4] = nrays; o[5] = fp_paths;
+    o[6] = 0; o[7] = fp_raymax;
+  }
+#endif
+#undef FPROF
 }
 
 }  // namespace rtd
