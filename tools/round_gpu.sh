@@ -14,3 +14,6 @@ python3 tools/summarize_profile.py gpurun_out/prof $TAG \
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 cp profiles/${TAG}_* profiles/pmc_C3.json gpurun_out/profiles/
+timeout -k 10 300 python3 tools/interactive_demo.py --config C3 --frames 60 --out gpurun_out/interactive > gpurun_out/interactive.log 2>&1 || { echo "interactive failed"; tail -5 gpurun_out/interactive.log; exit 1; }
+cp gpurun_out/interactive/C3_interactive.json gpurun_out/profiles/${TAG}_interactive.json
+tail -7 gpurun_out/interactive.log
