@@ -1230,7 +1230,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const unsigned int trace_grid1 = (unsigned)(c->n_cus * c->trace_bpc);
       static unsigned long long* d_wave_log = nullptr;  // debug only (RT_DEBUG_PASSES), never freed
       std::vector<unsigned long long> wave_log;
-      if (debug_passes && count) {
+      if (debug_passes) {
         if (!d_wave_log) HIPCHK(c, hipMalloc(&d_wave_log, (size_t)trace_grid * 4 * 4 * sizeof(unsigned long long)));
         wave_log.resize((size_t)trace_grid * 4 * 4);
       }
@@ -1253,7 +1253,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K.pool_chunk = c->pool_chunk;
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)g * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
-        WP.K.wave_log = (debug_passes && count) ? d_wave_log : nullptr;
+        WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds, or RT_TRACE_WAVELOG builds
         WP.S = c->wfg[g];
         WP.S.pix_xy = c->wf.pix_xy + w0;
         WP.S.pix_acc = c->wf.pix_acc + w0;

@@ -625,10 +625,17 @@ void wf_trace(const WFParams W) {
   unsigned long long v_rays = 0, v_ovf = 0;  // COUNT: rays, overflow-column pushes
   unsigned long long v_q[6] = {0, 0, 0, 0, 0, 0};  // COUNT: node visits by breadth-first index
   const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
+#ifdef RT_TRACE_WAVELOG  // development: per-wave start/end/iterations/rays of the timed kernel (RT_DEBUG_PASSES)
+  const unsigned long long wl_t0 = wall_clock64();
+  unsigned long long wl_it = 0, wl_rays = 0;
+#endif
   const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
 
   while (true) {
     if (COUNT) v_iter++;
+#ifdef RT_TRACE_WAVELOG
+    wl_it++;
+#endif
     // ---- refill idle lanes from the wave's pool.  One counter serves the whole chip and a
     // single atomic address sustains only ~90 atomics/us, so the pool is claimed in big chunks
     // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
@@ -786,6 +793,9 @@ void wf_trace(const WFParams W) {
       }
     }
     if (busy && finished) {
+#ifdef RT_TRACE_WAVELOG
+      wl_rays++;
+#endif
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
       if (COUNT) {
         if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
@@ -800,6 +810,15 @@ void wf_trace(const WFParams W) {
       busy = false;
     }
   }
+#ifdef RT_TRACE_WAVELOG
+  if (!COUNT && P.wave_log) {
+    for (int off = 32; off > 0; off >>= 1) wl_rays += __shfl_xor(wl_rays, off);
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long* wv = P.wave_log + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+      wv[0] = wl_t0; wv[1] = wall_clock64(); wv[2] = wl_it; wv[3] = wl_rays;
+    }
+  }
+#endif
   if (COUNT) {
     if (P.wave_log) {
       unsigned long long r = v_rays;
