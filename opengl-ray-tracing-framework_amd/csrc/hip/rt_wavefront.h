@@ -331,9 +331,7 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
 
 // one triangle (RT:241-299, R1); true when it becomes the closest hit
 template <bool WIDE>
-RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
-  const uint32_t off = (uint32_t)i * 48u;
-  const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
+RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d());
@@ -357,6 +355,12 @@ RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   L.besttri = i;
   L.bestt = t;
   return true;
+}
+template <bool WIDE>
+RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
+  const uint32_t off = (uint32_t)i * 48u;
+  const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
+  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc);
 }
 
 RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
@@ -406,27 +410,25 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
 }
 
 // 4-wide node L.cur: the four (grand)child boxes of the binary subtree it replaces, each with
-// the reference's slab test; survivors sorted by entry distance, nearest entered, rest stacked
-RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
-  const uint32_t off = (uint32_t)L.cur << 7;
-  // t0 / t1 of RT:312-313 for the four children; the box is hit iff t1 >= t0 && t1 > 0,
-  // which is exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
-  const int4 rf = ld<int4>(P.qnodes, off + 96u);
-  const float lim = cull ? cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz) : __int_as_float(0x7f800000);
-  float k[4];
-  int r[4];
+// the reference's slab test; survivors sorted by entry distance, nearest entered, rest stacked.
+// Split in parts: the box tests (tl_qnode_keys, planes given), the sort + push (tl_qnode_push),
+// so the finisher can fetch the node before its triangle test (tl_dual_load) while wf_trace
+// keeps the fetch inside each branch (fewer live registers at 64 VGPRs).
+// t0 / t1 of RT:312-313 for the four children; the box is hit iff t1 >= t0 && t1 > 0, which is
+// exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
+RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4 rf, const float4 p0, const float4 p1,
+                       const float4 p2, const float4 p3, const float4 p4, const float4 p5, float (&k)[4], int (&r)[4]) {
+  const float lim = cull ? cull_limit(L.best, cull_eps, L.ix, L.iy, L.iz) : __int_as_float(0x7f800000);
   auto keep = [&](int c, float t0, float t1, int ref) {
     const bool ok = t1 >= t0 && t1 > 0.0f && !(t0 > lim);
     k[c] = ok ? t0 : __int_as_float(0x7f800000);
     r[c] = ok ? ref : Q_EMPTY;
   };
   if (L.finite) {
-    // near / far planes chosen per ray by the load offsets; children in pairs with packed
-    // fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations, two at a time)
-    const float4 nx = ld<float4>(P.qnodes, off + L.offNx), ny = ld<float4>(P.qnodes, off + L.offNy),
-                 nz = ld<float4>(P.qnodes, off + L.offNz);
-    const float4 fx = ld<float4>(P.qnodes, off + (48 - L.offNx)), fy = ld<float4>(P.qnodes, off + (80 - L.offNy)),
-                 fz = ld<float4>(P.qnodes, off + (112 - L.offNz));
+    // near / far planes chosen per ray by the load offsets (p0..p5 = near x, y, z, far x, y, z);
+    // children in pairs with packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
+    // operations, two at a time)
+    const float4 nx = p0, ny = p1, nz = p2, fx = p3, fy = p4, fz = p5;
     const v2f ox = {L.ox, L.ox}, oy = {L.oy, L.oy}, oz = {L.oz, L.oz};
     const v2f ix = {L.ix, L.ix}, iy = {L.iy, L.iy}, iz = {L.iz, L.iz};
     const v2f nx01 = (v2f{nx.x, nx.y} - ox) * ix, ny01 = (v2f{ny.x, ny.y} - oy) * iy, nz01 = (v2f{nz.x, nz.y} - oz) * iz;
@@ -437,10 +439,9 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
     keep(1, max_(nx01.y, max_(ny01.y, nz01.y)), min_(fx01.y, min_(fy01.y, fz01.y)), rf.y);
     keep(2, max_(nx23.x, max_(ny23.x, nz23.x)), min_(fx23.x, min_(fy23.x, fz23.x)), rf.z);
     keep(3, max_(nx23.y, max_(ny23.y, nz23.y)), min_(fx23.y, min_(fy23.y, fz23.y)), rf.w);
-  } else {  // a direction component is exactly 0: the literal slab (0 * inf -> NaN cases)
-    const float4 lx = ld<float4>(P.qnodes, off), ly = ld<float4>(P.qnodes, off + 16u),
-                 lz = ld<float4>(P.qnodes, off + 32u), hx = ld<float4>(P.qnodes, off + 48u),
-                 hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
+  } else {  // a direction component is exactly 0: the literal slab (0 * inf -> NaN cases);
+            // p0..p5 = lo x, y, z, hi x, y, z
+    const float4 lx = p0, ly = p1, lz = p2, hx = p3, hy = p4, hz = p5;
     auto generic = [&](int c, float ax, float ay, float az, float bx, float by, float bz, int ref) {
       const f3 f = (mk3(bx, by, bz) - L.o()) * L.inv();
       const f3 n = (mk3(ax, ay, az) - L.o()) * L.inv();
@@ -452,6 +453,8 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
     generic(2, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, rf.z);
     generic(3, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, rf.w);
   }
+}
+RTD void tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, float (&k)[4], int (&r)[4]) {
   const int n = (r[0] != Q_EMPTY) + (r[1] != Q_EMPTY) + (r[2] != Q_EMPTY) + (r[3] != Q_EMPTY);
   // valid children sort ahead of empty slots unless a valid entry key is +inf (degenerate)
   const bool ordered = !((r[0] != Q_EMPTY && !(k[0] < INFINITY)) || (r[1] != Q_EMPTY && !(k[1] < INFINITY)) ||
@@ -486,6 +489,49 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   L.cur = r[0];
   L.haveCur = r[0] != Q_EMPTY || tl_pop(P, L, S, cull);
 }
+RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+  const uint32_t off = (uint32_t)L.cur << 7;
+  const int4 rf = ld<int4>(P.qnodes, off + 96u);
+  float k[4];
+  int r[4];
+  if (L.finite) {
+    const float4 nx = ld<float4>(P.qnodes, off + L.offNx), ny = ld<float4>(P.qnodes, off + L.offNy),
+                 nz = ld<float4>(P.qnodes, off + L.offNz);
+    const float4 fx = ld<float4>(P.qnodes, off + (48 - L.offNx)), fy = ld<float4>(P.qnodes, off + (80 - L.offNy)),
+                 fz = ld<float4>(P.qnodes, off + (112 - L.offNz));
+    tl_qnode_keys(L, cull, P.cull_eps, rf, nx, ny, nz, fx, fy, fz, k, r);
+  } else {
+    const float4 lx = ld<float4>(P.qnodes, off), ly = ld<float4>(P.qnodes, off + 16u),
+                 lz = ld<float4>(P.qnodes, off + 32u), hx = ld<float4>(P.qnodes, off + 48u),
+                 hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
+    tl_qnode_keys(L, cull, P.cull_eps, rf, lx, ly, lz, hx, hy, hz, k, r);
+  }
+  tl_qnode_push(P, L, S, cull, k, r);
+}
+// the node fetch alone (the finisher issues it before its triangle test): rf + six planes, near /
+// far for a finite 1/d, lo / hi otherwise (tl_start's offsets cover both)
+struct QLoad {
+  int4 rf;
+  float4 p[6];
+};
+RTD QLoad tl_qnode_load(const KParams& P, const TraceLane& L) {
+  const uint32_t off = (uint32_t)L.cur << 7;
+  QLoad q;
+  q.rf = ld<int4>(P.qnodes, off + 96u);
+  q.p[0] = ld<float4>(P.qnodes, off + L.offNx);
+  q.p[1] = ld<float4>(P.qnodes, off + L.offNy);
+  q.p[2] = ld<float4>(P.qnodes, off + L.offNz);
+  q.p[3] = ld<float4>(P.qnodes, off + (48 - L.offNx));
+  q.p[4] = ld<float4>(P.qnodes, off + (80 - L.offNy));
+  q.p[5] = ld<float4>(P.qnodes, off + (112 - L.offNz));
+  return q;
+}
+RTD void tl_qnode_calc(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, const QLoad& q) {
+  float k[4];
+  int r[4];
+  tl_qnode_keys(L, cull, P.cull_eps, q.rf, q.p[0], q.p[1], q.p[2], q.p[3], q.p[4], q.p[5], k, r);
+  tl_qnode_push(P, L, S, cull, k, r);
+}
 
 // start a ray on a lane whose origin, direction and anyhit are set: 1/d, plane offsets, root
 template <bool WIDE>
@@ -494,9 +540,10 @@ RTD void tl_start(const KParams& P, TraceLane& L) {
   // finite 1/d: per axis (lo-o)*inv <= (hi-o)*inv exactly when inv > 0 (rounding is
   // monotone), so the slab min/max of RT:309-310 is a fixed choice of plane per ray
   L.finite = fabs_(L.ix) < INFINITY && fabs_(L.iy) < INFINITY && fabs_(L.iz) < INFINITY;
-  L.offNx = L.ix > 0.0f ? 0 : 48;
-  L.offNy = L.iy > 0.0f ? 16 : 64;
-  L.offNz = L.iz > 0.0f ? 32 : 80;
+  // (a ray with a zero direction component reads lo / hi: offsets 0, 16, 32 / 48, 64, 80)
+  L.offNx = (L.ix > 0.0f || !L.finite) ? 0 : 48;
+  L.offNy = (L.iy > 0.0f || !L.finite) ? 16 : 64;
+  L.offNz = (L.iz > 0.0f || !L.finite) ? 32 : 80;
   L.best = INF;
   L.besttri = -1;
   L.bestt = 0.0f;
@@ -531,6 +578,58 @@ RTD bool tl_dual_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool
     }
   }
   return finished || (!L.haveCur && L.tri_i >= L.tri_end);
+}
+
+// Fetch half of one dual step: the triangle's 48 B and the node's 112 B of lane ray L (when it
+// has them to do), before either test
+struct DualLoad {
+  float4 A, B, Cc;
+  QLoad q;
+  bool doTri, doNode;
+};
+RTD DualLoad tl_dual_load(const KParams& P, const TraceLane& L, bool active) {
+  DualLoad d;
+  d.doTri = active && L.tri_i < L.tri_end;
+  d.doNode = active && L.haveCur && !ref_is_leaf(L.cur);
+  d.A = d.B = d.Cc = make_float4(0, 0, 0, 0);
+  if (d.doTri) {
+    const uint32_t off = (uint32_t)L.tri_i * 48u;
+    d.A = ld<float4>(P.tri, off);
+    d.B = ld<float4>(P.tri, off + 16u);
+    d.Cc = ld<float4>(P.tri, off + 32u);
+  }
+  if (d.doNode) d.q = tl_qnode_load(P, L);
+  return d;
+}
+// ... and the test half: the same steps as tl_dual_step (4-wide tree); true when the ray is done
+RTD bool tl_dual_calc(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull, const DualLoad& d) {
+  bool finished = false;
+  if (d.doTri) {
+    if (tl_triangle_calc<true>(P, L, L.tri_i, d.A, d.B, d.Cc) && L.anyhit) finished = true;
+    L.tri_i++;
+    if (finished) L.tri_end = L.tri_i;
+  }
+  if (!finished && L.haveCur) {
+    if (!d.doNode) {  // a leaf: taken once the triangle cursor is free
+      if (L.tri_i >= L.tri_end) {
+        L.tri_i = leaf_first(L.cur);
+        L.tri_end = L.tri_i + leaf_count(L.cur);
+        L.haveCur = tl_pop(P, L, TS, cull);
+      }
+    } else {
+      tl_qnode_calc(P, L, TS, cull, d.q);
+    }
+  }
+  return finished || (!L.haveCur && L.tri_i >= L.tri_end);
+}
+// the finisher's traversal step: both fetches first, then both tests, one memory round trip per
+// step instead of two.  It holds ~40 more values in flight than wf_trace's 64-VGPR budget allows
+// (issuing both together there cost 7% at 5 instead of 8 waves/SIMD); the finisher's latency-bound
+// waves have registers to spare (C3 1080p single frames -2.2%).  The binary tree keeps tl_dual_step.
+template <bool WIDE>
+RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull) {
+  if (!WIDE) return tl_dual_step<WIDE>(P, L, TS, cull);
+  return tl_dual_calc(P, L, TS, cull, tl_dual_load(P, L, true));
 }
 
 #ifndef RT_TRACE_WPE
@@ -1432,7 +1531,7 @@ void wf_finish(const WFParams W) {
       const unsigned long long tr = __ballot(st == FS_TRACE);
       if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
       FPROF(fp_it++; if (st == FS_TRACE) fp_ray++;)
-      if (st == FS_TRACE && (!P.has_scene || tl_dual_step<WIDE>(P, L, TS, cull))) {
+      if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
         nrays++;
         if (contNext) begin_rays(false, true);
