@@ -330,8 +330,12 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
 }
 
 // one triangle (RT:241-299, R1); true when it becomes the closest hit
+// anyw (wave-uniform): every busy lane of the wave traces an any-hit (shadow) ray, whose best stays
+// +inf until the first hit ends it: the closest-hit bound and compare are skipped (scalar branch);
+// a hit at dist == best = +inf stays rejected by the tie rule, as for a closest-hit ray
 template <bool WIDE>
-RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
+RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc,
+                          bool anyw = false) {
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d());
@@ -341,26 +345,31 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   // ~2^-21 of num / dn (|dn| >= 1e-5, no denormals), so outside these margins the exact t
   // fails RT:268 or the closest-hit test for certain.  NaN never rejects.
   const float qa = num * __builtin_amdgcn_rcpf(dn);
-  if (qa < 0.0005f * (1.0f - 0x1p-16f) || qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
+  if (qa < 0.0005f * (1.0f - 0x1p-16f)) return false;
+  if (!anyw && qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
   const float t = num / dot(L.d(), ng);                                // RT:265
   const float dist = t - 0.00001f;
-  if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
+  if (anyw) {
+    if (!(t >= 0.0005f && dist < INF)) return false;                   // RT:268 with best = +inf
+  } else if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) {
+    return false;                                                      // RT:268, RT:328/356
+  }
   const f3 Pp = L.o() + L.d() * t;
   const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
   const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
   const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
   if (!((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0))) return false;
-  if (WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
+  if (!anyw && WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
   L.best = dist;
   L.besttri = i;
   L.bestt = t;
   return true;
 }
 template <bool WIDE>
-RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
+RTD bool tl_triangle(const KParams& P, TraceLane& L, int i, bool anyw = false) {
   const uint32_t off = (uint32_t)i * 48u;
   const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
-  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc);
+  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc, anyw);
 }
 
 RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
@@ -420,7 +429,7 @@ RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4
                        const float4 p2, const float4 p3, const float4 p4, const float4 p5, float (&k)[4], int (&r)[4]) {
   const float lim = cull ? cull_limit(L.best, cull_eps, L.ix, L.iy, L.iz) : __int_as_float(0x7f800000);
   auto keep = [&](int c, float t0, float t1, int ref) {
-    const bool ok = t1 >= t0 && t1 > 0.0f && !(t0 > lim);
+    const bool ok = t1 >= t0 && t1 > 0.0f && (!cull || !(t0 > lim));
     k[c] = ok ? t0 : __int_as_float(0x7f800000);
     r[c] = ok ? ref : Q_EMPTY;
   };
@@ -649,6 +658,15 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
 #endif
+#ifndef RT_QUEUE_KIND_SEG  // wf_shade queues each block's shadow rays ahead of its continuations:
+                           // +0.4% C3, +1.0% C4 (tools/ab_proc.py, 3 rounds)
+#define RT_QUEUE_KIND_SEG 1
+#endif
+#ifndef RT_ANYHIT_WAVE  // waves whose busy lanes all trace shadow rays skip the closest-hit work:
+                        // measured -1.8% (C3) / -1.6% (C4) against the same queues without it (the
+                        // per-iteration ballot and scalar branches cost more than the VALU saved)
+#define RT_ANYHIT_WAVE 0
+#endif
 #ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed)
 #define RT_STATIC_FRAC 4
 #endif
@@ -789,10 +807,15 @@ void wf_trace(const WFParams W) {
     bool finished = false;
     if (MODE == TM_DUAL) {
       if (COUNT) { v_itN++; v_itT++; }
+      // every busy lane of the wave traces an any-hit (shadow) ray: best stays +inf until the hit
+      // that ends the ray, so culling drops nothing and the closest-hit bounds of the triangle test
+      // are moot; skipped behind scalar branches (wf_shade queues a block's shadow rays together)
+      const bool anyw = RT_ANYHIT_WAVE && __all(!busy || L.anyhit);
+      const bool cl = cull && !anyw;
       if (busy) {
         if (L.tri_i < L.tri_end) {
           if (COUNT) { v_tri++; ray_steps++; }
-          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+          if (tl_triangle<WIDE>(P, L, L.tri_i++, anyw) && L.anyhit) {
             finished = true;
             L.tri_end = L.tri_i;
           }
@@ -803,7 +826,7 @@ void wf_trace(const WFParams W) {
               if (COUNT) { v_leaf++; v_park++; }
               L.tri_i = leaf_first(L.cur);
               L.tri_end = L.tri_i + leaf_count(L.cur);
-              L.haveCur = tl_pop(P, L, TS, cull);
+              L.haveCur = tl_pop(P, L, TS, cl);
             }
           } else {
             if (COUNT) {
@@ -814,8 +837,8 @@ void wf_trace(const WFParams W) {
               }
             }
             const int sp0 = L.sp;
-            if (WIDE) tl_qnode(P, L, TS, cull);
-            else tl_node(P, L, TS, cull);
+            if (WIDE) tl_qnode(P, L, TS, cl);
+            else tl_node(P, L, TS, cl);
             if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
           }
         }
@@ -1342,7 +1365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __shared__ int la[256 * SH_SUB];
   __shared__ int lsort[256 * SH_SUB];  // the block's paths, grouped by shade_key
   __shared__ unsigned int lhist[SH_KEYS], lofs[SH_KEYS];
-  __shared__ unsigned int lc[4];  // queue count, active count, queue base, active base
+  __shared__ unsigned int lc[5];  // queue count (shadow rays), active count, queue base, active base, continuations
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
@@ -1363,7 +1386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   // utilisation ~0.8) loses more than it gains (measured on C3, 64 frames in flight).
   const unsigned int nblk = min(256u * SH_SUB, na - base);
   if (threadIdx.x < SH_KEYS) lhist[threadIdx.x] = 0u;
-  if (threadIdx.x == 0) lc[0] = lc[1] = 0u;
+  if (threadIdx.x == 0) lc[0] = lc[1] = lc[4] = 0u;
   __syncthreads();
 #if RT_SH_SORT_REL
   // sort only passes holding at least a quarter of the group's path slots (in practice pass 1,
@@ -1408,20 +1431,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     int path = live ? lsort[jj] : 0;
     const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
+#if RT_QUEUE_KIND_SEG
+    // shadow rays from the front of the block's staging list, continuations from the back: the
+    // block's queue run is [shadow rays][continuations], so a trace wave's claim is mostly one
+    // kind (RT_ANYHIT_WAVE)
+    const unsigned int qs = wave_lds_append(&lc[0], qShadow ? 1u : 0u);
+    const unsigned int qc = wave_lds_append(&lc[4], qCont ? 1u : 0u);
+    if (qShadow) lq[qs] = (path << 1) | 1;
+    if (qCont) lq[2 * 256 * SH_SUB - 1 - qc] = path << 1;
+#else
     const unsigned int qs = wave_lds_append(&lc[0], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u));
     if (qShadow) lq[qs] = (path << 1) | 1;
     if (qCont) lq[qs + (qShadow ? 1u : 0u)] = path << 1;
+#endif
     const unsigned int ai = wave_lds_append(&lc[1], keep ? 1u : 0u);
     if (keep) la[ai] = path;
     SHP_MARK(4)
   }
   __syncthreads();
+#if RT_QUEUE_KIND_SEG
+  if (threadIdx.x == 0) {
+    lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[out], lc[0] + lc[4]) : 0u;
+    lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
+  }
+  __syncthreads();
+  for (unsigned int j = threadIdx.x; j < lc[0] + lc[4]; j += 256u)
+    S.queue[out][lc[2] + j] = j < lc[0] ? lq[j] : lq[2 * 256 * SH_SUB - 1 - (j - lc[0])];
+#else
   if (threadIdx.x == 0) {
     lc[2] = lc[0] ? atomicAdd(&S.cnt[out], lc[0]) : 0u;
     lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
   }
   __syncthreads();
   for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue[out][lc[2] + j] = lq[j];
+#endif
   for (unsigned int j = threadIdx.x; j < lc[1]; j += 256u) S.active[out][lc[3] + j] = la[j];
   __syncthreads();
   SHP_MARK(5)
