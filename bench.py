@@ -382,6 +382,9 @@ def main(argv=None) -> int:
     base = (warm + steps) * F
     single = {}
     if n_single > 0:
+        # longest-first work order from one probe frame (rt_order_work; results unchanged): the
+        # costliest 64-pixel blocks are queued first, so a one-frame pass ends on cheap blocks
+        r.order_work(fp, ro[base:base + 1])
         r.render_async(fp, ro[base:base + 1])
         r.synchronize()
         t1 = time.perf_counter()

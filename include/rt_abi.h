@@ -146,6 +146,13 @@ int rt_get_tile_owners(const rt_ctx* ctx, int32_t* owner, int32_t n_tiles);
  * the accumulation are left as they were; the stats counters include the probe frames. */
 int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
                   uint64_t* costs);
+/* Longest-first work order (no GL counterpart: the rasteriser schedules fragments itself).  Renders
+ * n_frames as a cost probe (as rt_tile_costs, state left unchanged), then reorders this ctx's pixel
+ * list by whole 64-pixel blocks (an 8x8 block stays one wave) in descending cost, so the blocks
+ * whose rays cost most are queued first and a pass's tail is the cheap blocks.  Results are
+ * unchanged (pixels are independent; the accumulation keeps its layout); rt_resize and
+ * rt_set_tile_owners restore the natural order. */
+int rt_order_work(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames);
 /* Path-state budget in pixel-frames (208 B each): frames in flight per launch = slots / pixels of
  * this rank, at most RT_MAX_FRAMES_PER_LAUNCH.  0 = RT_MAX_SLOTS from the environment or the
  * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL

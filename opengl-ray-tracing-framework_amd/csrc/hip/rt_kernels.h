@@ -39,6 +39,7 @@ struct KParams {
   int W, H, tile_w, tile_h, tiles_x, rank, world;
   const int* __restrict__ tile_ids;   // global tile id of each local tile (rt_set_tile_owners)
   unsigned long long* __restrict__ tile_cost;  // rt_tile_costs probe: per local tile (else null)
+  int cost_blocks;                  // tile_cost indexed by 64-item work block (rt_order_work) instead of tile
   unsigned int n_work;
   const GNode* __restrict__ nodes;  // binary tree; GNode.ref.z = DFS rank of the first leaf on the right
   int root, has_scene, stack_entries;

@@ -99,6 +99,7 @@ struct rt_ctx {
   int2* d_tile_src = nullptr;      // tile_src on the device (rt_assemble_kernel)
   unsigned long long* d_tile_cost = nullptr;  // rt_tile_costs: per local tile, during the probe only
   bool tile_cost_on = false;
+  bool cost_blocks = false;        // the probe counts per 64-item work block (rt_order_work)
   float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera)
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
@@ -1184,6 +1185,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.W = c->W; P.H = c->H; P.tile_w = c->tile_w; P.tile_h = c->tile_h; P.tiles_x = c->tiles_x;
     P.rank = c->rank; P.world = c->world; P.tile_ids = c->d_tile_ids;
     P.tile_cost = c->tile_cost_on ? c->d_tile_cost : nullptr;
+    P.cost_blocks = c->cost_blocks ? 1 : 0;
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
     P.qnodes = c->d_qnodes; P.qroot = c->qroot;
@@ -1523,10 +1525,10 @@ int rt_stats_reset(rt_ctx* c) {
 // the visit-counting trace, which adds every ray's node + triangle steps (+ RT_COST_PER_RAY) to
 // its tile's counter.  Integer counts of a deterministic render: the same on every rank and box.
 // LoopNum and the accumulation are restored afterwards; the stats counters include the probe.
-int rt_tile_costs(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, uint64_t* costs) {
-  if (!c || !fp || !rand_origin || !costs || n_frames <= 0) return RT_ERR_ARG;
-  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
-  if (c->local_tiles == 0) return RT_OK;
+// One probe render (COUNT build of wf_trace) whose per-ray traversal steps accumulate into n_bins
+// costs: per local tile, or per 64-item work block (blocks); accumulation and LoopNum restored.
+static int cost_probe(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, uint64_t* costs,
+                      size_t n_bins, bool blocks) {
   int rc = rt_synchronize(c);
   if (rc) return rc;
   HIPCHK(c, hipSetDevice(c->device));
@@ -1536,26 +1538,63 @@ int rt_tile_costs(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   HIPCHK(c, hipMemcpy(saved, c->d_accum, abytes, hipMemcpyDeviceToDevice));
   const int loop = c->loop_num;
   dfree(c->d_tile_cost);
-  hipError_t he = hipMalloc(&c->d_tile_cost, (size_t)c->local_tiles * sizeof(unsigned long long));
-  if (he == hipSuccess) he = hipMemset(c->d_tile_cost, 0, (size_t)c->local_tiles * sizeof(unsigned long long));
+  hipError_t he = hipMalloc(&c->d_tile_cost, n_bins * sizeof(unsigned long long));
+  if (he == hipSuccess) he = hipMemset(c->d_tile_cost, 0, n_bins * sizeof(unsigned long long));
   if (he != hipSuccess) {
     (void)hipFree(saved);
-    return fail(c, RT_ERR_HIP, std::string("rt_tile_costs: ") + hipGetErrorString(he));
+    return fail(c, RT_ERR_HIP, std::string("cost probe: ") + hipGetErrorString(he));
   }
   rt_frame_params q = *fp;
   q.flags = (q.flags | RT_FLAG_COUNT_VISITS) & ~RT_FLAG_MEGAKERNEL;
   c->tile_cost_on = true;
+  c->cost_blocks = blocks;
   rc = rt_render(c, &q, rand_origin, n_frames, nullptr);
   c->tile_cost_on = false;
+  c->cost_blocks = false;
   if (rc == RT_OK) {
-    he = hipMemcpy(costs, c->d_tile_cost, (size_t)c->local_tiles * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    he = hipMemcpy(costs, c->d_tile_cost, n_bins * sizeof(uint64_t), hipMemcpyDeviceToHost);
     if (he == hipSuccess) he = hipMemcpy(c->d_accum, saved, abytes, hipMemcpyDeviceToDevice);
-    if (he != hipSuccess) rc = fail(c, RT_ERR_HIP, std::string("rt_tile_costs: ") + hipGetErrorString(he));
+    if (he != hipSuccess) rc = fail(c, RT_ERR_HIP, std::string("cost probe: ") + hipGetErrorString(he));
   }
   (void)hipFree(saved);
   dfree(c->d_tile_cost);
   c->loop_num = loop;
   return rc;
+}
+
+int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames) {
+  if (!c || !fp || !rand_origin || n_frames <= 0) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  const size_t nv = (size_t)c->n_valid, nb = nv / 64;  // whole 64-item blocks (a partial one stays last)
+  if (nb < 2) return RT_OK;
+  std::vector<uint64_t> cost((nv + 63) / 64);
+  int rc = cost_probe(c, fp, rand_origin, n_frames, cost.data(), cost.size(), true);
+  if (rc) return rc;
+  std::vector<uint32_t> order(nb);
+  for (size_t b = 0; b < nb; b++) order[b] = (uint32_t)b;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+  // permute the pixel list (xy then accumulation index) by whole blocks: a wave keeps its 8x8
+  // block, and the blocks whose rays cost most are queued (and claimed) first
+  std::vector<unsigned int> pix(2 * nv), out(2 * nv);
+  HIPCHK(c, hipMemcpy(pix.data(), c->d_pix, 2 * nv * sizeof(unsigned int), hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < nb; k++)
+    for (size_t j = 0; j < 64; j++) {
+      out[k * 64 + j] = pix[(size_t)order[k] * 64 + j];
+      out[nv + k * 64 + j] = pix[nv + (size_t)order[k] * 64 + j];
+    }
+  for (size_t j = nb * 64; j < nv; j++) {
+    out[j] = pix[j];
+    out[nv + j] = pix[nv + j];
+  }
+  HIPCHK(c, hipMemcpy(c->d_pix, out.data(), 2 * nv * sizeof(unsigned int), hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+int rt_tile_costs(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, uint64_t* costs) {
+  if (!c || !fp || !rand_origin || !costs || n_frames <= 0) return RT_ERR_ARG;
+  if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
+  if (c->local_tiles == 0) return RT_OK;
+  return cost_probe(c, fp, rand_origin, n_frames, costs, (size_t)c->local_tiles, false);
 }
 
 int rt_render(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, int32_t n_frames, rt_stats* st) {

@@ -922,7 +922,7 @@ void wf_trace(const WFParams W) {
       if (COUNT) {
         if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
           const unsigned int w = (unsigned int)(entry >> 1) / (unsigned int)P.n_frames;
-          atomicAdd(&P.tile_cost[S.pix_acc[w] / (unsigned int)(P.tile_w * P.tile_h)],
+          atomicAdd(&P.tile_cost[P.cost_blocks ? w >> 6 : S.pix_acc[w] / (unsigned int)(P.tile_w * P.tile_h)],
                     (unsigned long long)(ray_steps + RT_COST_PER_RAY));
         }
         if (P.wave_log)  // RT_DEBUG_PASSES: steps-per-ray histogram by kind (16-step buckets)

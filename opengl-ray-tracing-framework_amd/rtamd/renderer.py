@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
-    "rt_tile_costs", "rt_set_finish",
+    "rt_tile_costs", "rt_set_finish", "rt_order_work",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -179,6 +179,8 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_set_max_paths.argtypes = [vp, C.c_uint64]
     if hasattr(L, "rt_set_finish"):  # (absent from older builds loaded for A/B timing)
         L.rt_set_finish.argtypes = [vp, C.c_int32, C.c_uint64]
+    if hasattr(L, "rt_order_work"):
+        L.rt_order_work.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32]
     L.rt_set_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
@@ -301,6 +303,13 @@ class Renderer:
         self._check(self._L.rt_tile_costs(self._h, C.byref(p), _fp(ro), len(ro),
                                           out.ctypes.data_as(C.POINTER(C.c_uint64))), "rt_tile_costs")
         return out[:n]
+
+    def order_work(self, params: FrameParams, rand_origins: Sequence[float]) -> None:
+        """rt_order_work: probe these frames' per-block costs and queue the costliest 64-pixel
+        blocks first (results unchanged; rt_resize restores the natural order)."""
+        ro = np.ascontiguousarray(rand_origins, np.float32)
+        p = params.to_c()
+        self._check(self._L.rt_order_work(self._h, C.byref(p), _fp(ro), len(ro)), "rt_order_work")
 
     # ------------------------------------------------------------------ frames
     def reset(self) -> None:

@@ -213,3 +213,27 @@ def test_path_budget_beyond_device_memory_falls_back(env_maps):
         finally:
             r.close()
     assert bit_mismatch(out[0], out[1])[0] == 0.0
+
+
+@pytest.mark.parametrize("name", ["C3", "C4"])
+def test_longest_first_work_order_keeps_the_image(gpu_renderer, env_maps, name):
+    """rt_order_work reorders the pixel list by 64-pixel blocks of descending probe cost: every
+    later frame still equals the oracle bit for bit, one and several frames per call, and the
+    probe leaves LoopNum and the accumulation as they were."""
+    sd = cf.config_scene(name)
+    W, H = 96, 72
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 3)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    r = gpu_renderer
+    r.set_scene_soa(sd.soa, sd.nodes)
+    r.set_env(*env_maps)
+    r.resize(W, H)
+    r.order_work(fp, cf.rand_origins(1))
+    assert r.loop_num == 0
+    r.reset_stats()  # (the probe frame's rays are counted too)
+    r.render(fp, ro[:1])
+    st = r.render(fp, ro[1:])
+    img = r.read_accum()
+    assert bit_mismatch(img, ref)[0] == 0.0
+    assert st["rays"] == cnt["rays"]

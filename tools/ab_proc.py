@@ -43,6 +43,8 @@ if a.one is not None:
         r.set_max_paths(a.frames * W * H)
     fp = cf.frame_params(W, H)
     ro = cf.rand_origins(a.frames)
+    if os.environ.get("RT_AB_ORDER"):  # rt_order_work from one probe frame before timing
+        r.order_work(fp, ro[:1])
     r.render(fp, ro)
     r.reset_stats()
     r.synchronize()
