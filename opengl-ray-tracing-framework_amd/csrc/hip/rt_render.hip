@@ -1570,9 +1570,15 @@ int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   std::vector<uint64_t> cost((nv + 63) / 64);
   int rc = cost_probe(c, fp, rand_origin, n_frames, cost.data(), cost.size(), true);
   if (rc) return rc;
-  std::vector<uint32_t> order(nb);
-  for (size_t b = 0; b < nb; b++) order[b] = (uint32_t)b;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+  std::vector<uint32_t> sorted(nb), order;
+  for (size_t b = 0; b < nb; b++) sorted[b] = (uint32_t)b;
+  std::stable_sort(sorted.begin(), sorted.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+  // dealt round-robin into the n_groups ranges a one-frame call splits the pixels into, so every
+  // group gets an even share of the costly blocks, each in descending order
+  const int G = std::max(1, c->n_groups);
+  order.reserve(nb);
+  for (int g = 0; g < G; g++)
+    for (size_t k = (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);
   // permute the pixel list (xy then accumulation index) by whole blocks: a wave keeps its 8x8
   // block, and the blocks whose rays cost most are queued (and claimed) first
   std::vector<unsigned int> pix(2 * nv), out(2 * nv);
