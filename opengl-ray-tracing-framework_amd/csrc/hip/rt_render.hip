@@ -1503,7 +1503,7 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
 #ifdef RT_SHADE_PROF  // development variant: wave cycles per wf_shade phase (stats 16..21)
   unsigned long long ph[6];
   HIPCHK(c, hipMemcpy(ph, c->d_stats + 16, sizeof(ph), hipMemcpyDeviceToHost));
-  fprintf(stderr, "[shade-prof] sort %llu consume %llu nee %llu sample %llu store %llu flush %llu\n",
+  fprintf(stderr, "[shade-prof] sort %llu consume %llu bounce %llu store %llu append %llu flush %llu\n",
           ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
 #endif
   return RT_OK;

@@ -1028,9 +1028,13 @@ constexpr int SH_SUB = RT_SH_SUB;
 #ifdef RT_SHADE_PROF  // development variant: wave cycles per phase -> stats[16..21]
 #define SHP_DECL unsigned long long shp[6] = {0, 0, 0, 0, 0, 0}, shp_t = clock64();
 #define SHP_MARK(i) { const unsigned long long _n = clock64(); shp[i] += _n - shp_t; shp_t = _n; }
+#define SHP_PARAMS , unsigned long long (&shp)[6], unsigned long long& shp_t
+#define SHP_ARGS , shp, shp_t
 #else
 #define SHP_DECL
 #define SHP_MARK(i)
+#define SHP_PARAMS
+#define SHP_ARGS
 #endif
 
 // One path's shade step (the body of wf_shade, shared with wf_finish): consume the traced results
@@ -1042,7 +1046,7 @@ struct ShadeOut {
 };
 template <bool BSDF>
 RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
-                        unsigned long long& nsamples) {
+                        unsigned long long& nsamples SHP_PARAMS) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   bool doFinish = false, doBounce = false;
@@ -1179,6 +1183,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
   }
 
+  SHP_MARK(1)
   // ------------------------------------------------------------- next bounce
   f3 cnee = splat(0.0f), cmed = splat(0.0f);
   uint32_t nflags = 0;
@@ -1325,6 +1330,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
   }
 
+  SHP_MARK(2)
   // ----------------------------------------------------------- progressive blend
   if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
     S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
@@ -1354,6 +1360,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
     }
   }
+  SHP_MARK(3)
   return ShadeOut{qShadow, qCont};
 }
 
@@ -1429,7 +1436,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
-    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
+    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples SHP_ARGS);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
 #if RT_QUEUE_KIND_SEG
     // shadow rays from the front of the block's staging list, continuations from the back: the
@@ -1520,6 +1527,7 @@ void wf_finish(const WFParams W) {
   TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
   unsigned long long nrays = 0, nsamples = 0;
+  SHP_DECL  // (RT_SHADE_PROF builds: shade_path's phase marks, not reported for the finisher)
   // lane state: no path / tracing the path's queued rays / rays done, waiting for its shade step
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
@@ -1584,7 +1592,7 @@ void wf_finish(const WFParams W) {
     if (__any(st == FS_SHADE)) {
       FPROF(fp_sh++;)
       const bool sh = st == FS_SHADE;
-      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
+      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples SHP_ARGS);
       if (sh) {
         if (o.qShadow || o.qCont) {
           st = FS_TRACE;
