@@ -1497,11 +1497,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // steps at ~1 us each, whatever the pass size), so the late passes of a single 1080p frame cost
 // ~0.2 ms each while tracing only thousands of rays.  After pass F-1's shade, wf_finish gives each
 // remaining path one lane, which traces the path's queued rays (shadow, then continuation: the
-// same dual-cursor step as wf_trace) and runs the path's shade step (shade_path, as wf_shade),
-// bounce after bounce until the path ends; a lane whose path ended takes the next one from the
-// active list.  A wave's chain is then its longest remaining path instead of the sum over passes
-// of each pass's longest ray.  Same device functions in the same order per path: the image and
-// the ray count are unchanged.
+// dual-cursor steps of wf_trace, fetching triangle and node together, tl_step_prefetch) and runs
+// the path's shade step (shade_path, as wf_shade), bounce after bounce until the path ends; a
+// lane whose path ended takes the next one from the active list, and a wave runs shade steps in
+// batches of RT_FINISH_SHADE_MIN ready lanes (or when no lane is tracing), so a lane does not wait
+// for the wave's slowest ray of every bounce.  Same device functions in the same order per path:
+// the image and the ray count are unchanged.  (Per-wave profile, RT_FINISH_PROF: the finisher is
+// bound by latency at 2 waves/SIMD over ~80 paths per wave, not by single long rays.)
 #ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
 #define RT_FINISH_SHADE_MIN 16
 #endif
