@@ -73,6 +73,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--single-frames", type=int, default=64,
                     help="frames rendered one per rt_render call after the timed region (ms_per_frame_single)")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="one-frame calls in flight together for ms_per_frame_single (rt_set_pipeline; 1: off)")
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the interleaved t %% N tile map instead of the cost-balanced one")
@@ -382,16 +384,22 @@ def main(argv=None) -> int:
     base = (warm + steps) * F
     single = {}
     if n_single > 0:
-        # longest-first work order from one probe frame (rt_order_work; results unchanged): the
-        # costliest 64-pixel blocks are queued first, so a one-frame pass ends on cheap blocks
-        r.order_work(fp, ro[base:base + 1])
-        r.render_async(fp, ro[base:base + 1])
-        r.synchronize()
-        t1 = time.perf_counter()
-        for k in range(n_single):
-            r.render_async(fp, ro[base + k:base + k + 1])
-        r.synchronize()
-        single["ms_per_frame_single"] = round((time.perf_counter() - t1) * 1e3 / n_single, 3)
+        # back-to-back one-frame calls, one call in flight at a time and then with frames in flight
+        # across calls (rt_set_pipeline: the GL driver's own frame queue; results unchanged)
+        for depth in (args.pipeline, 1) if args.pipeline > 1 else (1,):
+            r.set_pipeline(depth)
+            # longest-first work order from one probe frame (rt_order_work; results unchanged): the
+            # costliest 64-pixel blocks are queued first, so a one-frame pass ends on cheap blocks
+            r.order_work(fp, ro[base:base + 1])
+            r.render_async(fp, ro[base:base + 1])
+            r.synchronize()
+            t1 = time.perf_counter()
+            for k in range(n_single):
+                r.render_async(fp, ro[base + k:base + k + 1])
+            r.synchronize()
+            ms = round((time.perf_counter() - t1) * 1e3 / n_single, 3)
+            single["ms_per_frame_single" if depth > 1 or args.pipeline <= 1 else "ms_per_frame_single_one_in_flight"] = ms
+        single["single_frame_pipeline"] = max(1, args.pipeline)
         lat = []
         for k in range(min(16, n_single)):
             t2 = time.perf_counter()

@@ -164,6 +164,14 @@ int rt_set_max_paths(rt_ctx* ctx, uint64_t slots);
  * in one launch, one lane per path (results unchanged).  pass 0 disables it; defaults 2 and 8 Mi
  * slots (1080p: up to 8 frames per group).  RT_FLAG_NO_FINISH / RT_FLAG_FINISH override per call. */
 int rt_set_finish(rt_ctx* ctx, int32_t pass, uint64_t max_slots);
+/* Frames in flight across one-frame calls (the GL driver's own frame queue: main.cpp:175-251
+ * issues a draw per loop pass and glfwSwapBuffers does not wait for it to finish).  With depth
+ * >= 2, consecutive one-frame rt_render_async calls run on `depth` (at most 3) alternating
+ * internal streams with their own path state, so call k+1's early passes overlap call k's
+ * latency-bound last bounces.  Only call k+1's blend waits for the ctx stream (call k's blend and
+ * whatever the caller queued there since), and the ctx stream still joins every call at its end:
+ * results and ordering are those of depth 1.  Default 1; synchronises the ctx. */
+int rt_set_pipeline(rt_ctx* ctx, int32_t depth);
 
 /* Enqueue n_frames progressive frames (one randOrigin per frame) on the ctx stream.  Each
  * frame first applies main.cpp:175 (LoopNum++ unless it reached max_iterations). */

@@ -64,11 +64,15 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
-  // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table
-  int* h_ftab = nullptr;                      // [cap] loop_num then [cap] rand_origin bits
-  int* d_ftab = nullptr;
-  size_t ftab_cap = 0;
-  hipEvent_t ftab_event = nullptr;            // the last upload (the host table is reused after it)
+  // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table;
+  // ft[0] for batched calls, ft[1 + p] for pipelined one-frame calls on pipeline set p
+  struct FrameTable {
+    int* h = nullptr;                         // [cap] loop_num then [cap] rand_origin bits
+    int* d = nullptr;                         // + [cap][4] float2 Sobol pairs (wf_sobol)
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;                  // the last upload (the host table is reused after it)
+  };
+  FrameTable ft[5];
   int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
   int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
   int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
@@ -101,6 +105,7 @@ struct rt_ctx {
   bool tile_cost_on = false;
   bool cost_blocks = false;        // the probe counts per 64-item work block (rt_order_work)
   float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera)
+  int cam_sets = 1;                // camera tables in d_cam (one per pipeline set, n_valid each)
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
   size_t max_slots_req = 0;        // rt_set_max_paths (0: RT_MAX_SLOTS or the 320 Mi default)
@@ -109,6 +114,16 @@ struct rt_ctx {
   int finish_pass = 2;  // C3 1080p single frames: 1 / 2 / 3 -> 3.73 / 3.35 / 3.41 ms (off: 3.79)
   uint64_t finish_slots = uint64_t(8) << 20;
   int finish_bpc = 0;              // wf_finish blocks per CU
+  // Pipelined one-frame calls (rt_set_pipeline, depth D >= 2): one-frame call k runs as a single
+  // group on stream aux[1 + p], p = k mod D, with path-state set wfg[p], camera table p and frame
+  // table ft[1 + p], so call k+1's early passes fill the CUs that call k's latency-bound finisher
+  // leaves idle.  Only the blend waits for the caller's stream (history, frame order); the caller's
+  // stream still joins each call at its end.  set_free[p]: the last call on set p has finished;
+  // batch_done: the last batched (non-pipelined) call has finished.
+  int pipe_depth = 1;
+  int pipe_next = 0;
+  hipEvent_t set_free[MAX_GROUPS] = {};
+  hipEvent_t batch_done = nullptr;
 };
 
 namespace {
@@ -731,16 +746,21 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& a : c->aux) if (a) (void)hipStreamSynchronize(a);
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
+  if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
   dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   for (auto& a : c->aux) if (a) (void)hipStreamDestroy(a);
-  if (c->ftab_event) (void)hipEventDestroy(c->ftab_event);
-  if (c->h_ftab) (void)hipHostFree(c->h_ftab);
-  dfree(c->d_ftab);
+  for (auto& t : c->ft) {
+    if (t.ev) (void)hipEventDestroy(t.ev);
+    if (t.h) (void)hipHostFree(t.h);
+    dfree(t.d);
+  }
   dfree(c->d_pix);
   dfree(c->d_tile_ids);
   dfree(c->d_tile_src);
@@ -977,6 +997,8 @@ int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32
 // coherence) and the wavefront state sized for it.
 static int apply_tiling(rt_ctx* c, int width, int height, const rt_tiling& tl, std::vector<int32_t> owner) {
   HIPCHK(c, hipSetDevice(c->device));
+  // renders in flight read the buffers replaced below (the caller's stream joins every call)
+  if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
   // the old pixel lists / accumulation no longer describe the frame from here on: a failure
   // below leaves the context un-sized (rt_render_async then refuses) rather than half-resized
   c->frame_set = false;
@@ -1027,6 +1049,7 @@ static int apply_tiling(rt_ctx* c, int width, int height, const rt_tiling& tl, s
   const size_t nv = std::max<size_t>(1, xy.size());
   HIPCHK(c, hipMalloc(&c->d_pix, 2 * nv * sizeof(unsigned int)));
   HIPCHK(c, hipMalloc(&c->d_cam, nv * sizeof(float4)));
+  c->cam_sets = 1;
   if (!xy.empty()) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_pix + nv, acc.data(), acc.size() * 4, hipMemcpyHostToDevice));
@@ -1102,6 +1125,15 @@ int rt_set_finish(rt_ctx* c, int32_t pass, uint64_t max_slots) {
   return RT_OK;
 }
 
+int rt_set_pipeline(rt_ctx* c, int32_t depth) {
+  if (!c || depth < 1) return RT_ERR_ARG;
+  int rc = rt_synchronize(c);  // calls in flight keep the sets they were given
+  if (rc) return rc;
+  c->pipe_depth = std::min<int>(depth, rt_ctx::MAX_GROUPS - 1);  // streams aux[1 ..]
+  c->pipe_next = 0;
+  return RT_OK;
+}
+
 int rt_clear_accum(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   if (!c->frame_set) return fail(c, RT_ERR_STATE, "rt_resize first");
@@ -1131,39 +1163,73 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
   }
   // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12).
-  // The traced frames' (loopNum, randOrigin) go to a device table in one upload.
-  if (n_frames > 0 && (size_t)n_frames > c->ftab_cap) {
-    if (c->ftab_event) HIPCHK(c, hipEventSynchronize(c->ftab_event));
-    if (c->h_ftab) (void)hipHostFree(c->h_ftab);
-    c->h_ftab = nullptr;
-    dfree(c->d_ftab);
-    const size_t cap = std::max<size_t>(1024, (size_t)n_frames);
-    HIPCHK(c, hipHostMalloc((void**)&c->h_ftab, 2 * cap * sizeof(int)));
-    // device table: [cap] loop_num, [cap] rand_origin, then [cap][4] float2 Sobol pairs (wf_sobol)
-    HIPCHK(c, hipMalloc((void**)&c->d_ftab, 10 * cap * sizeof(int)));
-    c->ftab_cap = cap;
+  int n_trace_pre = 0;
+  for (int k = 0, ln = c->loop_num; k < n_frames; k++) {
+    if (fp->max_iterations == -1 || ln < fp->max_iterations) ln++;
+    if (fp->max_iterations == -1 || ln < fp->max_iterations) n_trace_pre++;
   }
-  if (!c->ftab_event) HIPCHK(c, hipEventCreateWithFlags(&c->ftab_event, hipEventDisableTiming));
-  HIPCHK(c, hipEventSynchronize(c->ftab_event));  // the previous call's upload has read h_ftab
+  // a pipelined one-frame call (rt_set_pipeline): see rt_ctx::pipe_depth
+  static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
+  const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
+  const bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && n_trace_pre > 0 &&
+                    n_trace_pre < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
+  const int pset = pipe ? c->pipe_next : 0;
+  hipStream_t ps = pipe ? c->aux[1 + pset] : c->stream;  // the stream that runs this call
+  hipEvent_t e_entry = nullptr;  // pipelined: the caller's stream at entry (the blend waits for it)
+  if (pipe) {
+    c->pipe_next = (c->pipe_next + 1) % pipe_sets;
+    if (!ps) {
+      HIPCHK(c, hipStreamCreateWithFlags(&c->aux[1 + pset], hipStreamNonBlocking));
+      ps = c->aux[1 + pset];
+    }
+    if (c->cam_sets < pipe_sets) {  // one camera table per set (a call may move the camera)
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      dfree(c->d_cam);
+      HIPCHK(c, hipMalloc(&c->d_cam, (size_t)std::max(1, c->n_valid) * pipe_sets * sizeof(float4)));
+      c->cam_sets = pipe_sets;
+      c->wf.cam = c->d_cam;
+    }
+    e_entry = take_event(c);
+    if (!e_entry) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+    HIPCHK(c, hipEventRecord(e_entry, c->stream));
+    // the set's previous call and the last batched call have finished with its state
+    if (c->set_free[pset]) HIPCHK(c, hipStreamWaitEvent(ps, c->set_free[pset], 0));
+    if (c->batch_done) HIPCHK(c, hipStreamWaitEvent(ps, c->batch_done, 0));
+  }
+  // The traced frames' (loopNum, randOrigin) go to a device table in one upload.
+  rt_ctx::FrameTable& T = c->ft[pipe ? 1 + pset : 0];
+  if (n_frames > 0 && (size_t)n_frames > T.cap) {
+    if (T.ev) HIPCHK(c, hipEventSynchronize(T.ev));
+    if (T.h) (void)hipHostFree(T.h);
+    T.h = nullptr;
+    if (T.d) HIPCHK(c, hipStreamSynchronize(c->stream));  // calls in flight read the old table
+    dfree(T.d);
+    const size_t cap = std::max<size_t>(pipe ? 16 : 1024, (size_t)n_frames);
+    HIPCHK(c, hipHostMalloc((void**)&T.h, 2 * cap * sizeof(int)));
+    // device table: [cap] loop_num, [cap] rand_origin, then [cap][4] float2 Sobol pairs (wf_sobol)
+    HIPCHK(c, hipMalloc((void**)&T.d, 10 * cap * sizeof(int)));
+    T.cap = cap;
+  }
+  if (!T.ev) HIPCHK(c, hipEventCreateWithFlags(&T.ev, hipEventDisableTiming));
+  HIPCHK(c, hipEventSynchronize(T.ev));  // the previous upload from this table has read T.h
   int n_traced = 0;
   for (int k = 0; k < n_frames; k++) {
     if (fp->max_iterations == -1 || c->loop_num < fp->max_iterations) c->loop_num++;
     if (!(fp->max_iterations == -1 || c->loop_num < fp->max_iterations)) continue;
-    c->h_ftab[n_traced] = c->loop_num;
-    memcpy(&c->h_ftab[c->ftab_cap + n_traced], &rand_origin[k], 4);
+    T.h[n_traced] = c->loop_num;
+    memcpy(&T.h[T.cap + n_traced], &rand_origin[k], 4);
     n_traced++;
   }
   if (n_traced > 0) {
-    HIPCHK(c, hipMemcpyAsync(c->d_ftab, c->h_ftab, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_ftab + c->ftab_cap, c->h_ftab + c->ftab_cap, (size_t)n_traced * sizeof(int),
-                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(T.d, T.h, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, ps));
+    HIPCHK(c, hipMemcpyAsync(T.d + T.cap, T.h + T.cap, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, ps));
   }
-  HIPCHK(c, hipEventRecord(c->ftab_event, c->stream));
-  const int* d_loop = c->d_ftab;
-  const float* d_ro = reinterpret_cast<const float*>(c->d_ftab + c->ftab_cap);
-  float2* d_sobol = reinterpret_cast<float2*>(c->d_ftab + 2 * c->ftab_cap);
+  HIPCHK(c, hipEventRecord(T.ev, ps));
+  const int* d_loop = T.d;
+  const float* d_ro = reinterpret_cast<const float*>(T.d + T.cap);
+  float2* d_sobol = reinterpret_cast<float2*>(T.d + 2 * T.cap);
   if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
-    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, c->stream, d_loop, d_sobol, n_traced);
+    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, d_loop, d_sobol, n_traced);
     HIPCHK(c, hipGetLastError());
   }
   int done = 0;
@@ -1207,7 +1273,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     const bool count = (fp->flags & RT_FLAG_COUNT_VISITS) != 0;
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (!e0 || !e1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
-    HIPCHK(c, hipEventRecord(e0, c->stream));
+    HIPCHK(c, hipEventRecord(e0, ps));
     if (fp->flags & RT_FLAG_MEGAKERNEL) {
       HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 4, c->stream));
       unsigned int max_blocks = (P.n_work + 255) / 256;
@@ -1223,9 +1289,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       // of fewer frames than groups (one frame per call: the reference's own usage) is split by
       // pixels instead (work items [w0, w1) each, all frames), so the groups' latency-bound late
       // passes still overlap each other
-      static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
-      const bool pix_split = pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
-      const int G = pix_split ? c->n_groups : std::min(c->n_groups, nf);
+      const bool pix_split = !pipe && pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
+      const int G = pipe ? 1 : pix_split ? c->n_groups : std::min(c->n_groups, nf);
       static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
       const unsigned int trace_grid = (unsigned)(c->n_cus * std::max(c->trace_bpc, c->trace_bpc0));
       const unsigned int trace_grid0 = (unsigned)(c->n_cus * c->trace_bpc0);
@@ -1253,27 +1318,29 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K.n_work = w1 - w0;
         WP.K.lds_entries = c->trace_lds_entries;
         WP.K.pool_chunk = c->pool_chunk;
-        WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)g * ovf_group : nullptr;
+        const int set = pipe ? pset : g;  // path-state set, overflow column, stream
+        float4* cam = c->wf.cam + (pipe ? (size_t)pset * (size_t)c->n_valid : 0);
+        WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)set * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
         WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds, or RT_TRACE_WAVELOG builds
-        WP.S = c->wfg[g];
+        WP.S = c->wfg[set];
         WP.S.pix_xy = c->wf.pix_xy + w0;
         WP.S.pix_acc = c->wf.pix_acc + w0;
-        WP.S.cam = c->wf.cam + w0;
+        WP.S.cam = cam + w0;
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
-        sg[g] = g == 0 ? c->stream : c->aux[g];
+        sg[g] = pipe ? ps : g == 0 ? c->stream : c->aux[g];
       }
       // camera directions of this call's pixels (every group reads them)
       rtd::WFParams WC = WG[0];
       WC.K.n_work = (unsigned)c->n_valid;
       WC.S.pix_xy = c->wf.pix_xy;
       WC.S.pix_acc = c->wf.pix_acc;
-      WC.S.cam = c->wf.cam;
+      WC.S.cam = WG[0].S.cam;
       hipLaunchKernelGGL(rtd::wf_camera, dim3(std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256))),
-                         dim3(256), 0, c->stream, WC);
+                         dim3(256), 0, ps, WC);
       HIPCHK(c, hipGetLastError());
       // aux streams start after everything already queued on the caller's stream
       if (G > 1) {
@@ -1436,6 +1503,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           HIPCHK(c, hipStreamWaitEvent(sg[g], prev_blend, 0));
           c->event_pool.push_back(prev_blend);
         }
+        if (e_entry) {  // pipelined: after the caller's work on the accumulation and the previous call
+          HIPCHK(c, hipStreamWaitEvent(sg[g], e_entry, 0));
+          c->event_pool.push_back(e_entry);  // reusable once the wait is enqueued
+          e_entry = nullptr;
+        }
         hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WP);
         HIPCHK(c, hipGetLastError());
         if (!pix_split && g + 1 < G) {
@@ -1454,7 +1526,17 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         c->event_pool.push_back(ej);
       }
     }
-    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventRecord(e1, ps));
+    if (pipe) {  // the caller's stream joins the call; the set is free again after it
+      if (c->set_free[pset]) c->event_pool.push_back(c->set_free[pset]);
+      c->set_free[pset] = take_event(c);
+      if (!c->set_free[pset]) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+      HIPCHK(c, hipEventRecord(c->set_free[pset], ps));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->set_free[pset], 0));
+    } else if (pipe_sets >= 2) {  // pipelined calls that follow start after this batch
+      if (!c->batch_done) HIPCHK(c, hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(c->batch_done, c->stream));
+    }
     c->events.push_back({e0, e1});
     c->launches++;
     int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents);
@@ -1575,7 +1657,8 @@ int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   std::stable_sort(sorted.begin(), sorted.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
   // dealt round-robin into the n_groups ranges a one-frame call splits the pixels into, so every
   // group gets an even share of the costly blocks, each in descending order
-  const int G = std::max(1, c->n_groups);
+  // (a pipelined one-frame call is one range: rt_set_pipeline)
+  const int G = (c->pipe_depth >= 2 && c->n_groups >= 2) ? 1 : std::max(1, c->n_groups);
   order.reserve(nb);
   for (int g = 0; g < G; g++)
     for (size_t k = (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);

@@ -36,7 +36,7 @@ ABI_SYMBOLS = (
     "rt_clear_accum", "rt_render_async", "rt_render", "rt_synchronize", "rt_stats_get", "rt_stats_reset",
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
-    "rt_tile_costs", "rt_set_finish", "rt_order_work",
+    "rt_tile_costs", "rt_set_finish", "rt_order_work", "rt_set_pipeline",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -181,6 +181,8 @@ def _bind(L: C.CDLL) -> C.CDLL:
         L.rt_set_finish.argtypes = [vp, C.c_int32, C.c_uint64]
     if hasattr(L, "rt_order_work"):
         L.rt_order_work.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32]
+    if hasattr(L, "rt_set_pipeline"):
+        L.rt_set_pipeline.argtypes = [vp, C.c_int32]
     L.rt_set_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
@@ -332,6 +334,10 @@ class Renderer:
         """rt_set_finish: end paths in the path-persistent finisher after pass `pass_ - 1` for frame
         groups of at most `max_slots` path slots (pass_ 0: never)."""
         self._check(self._L.rt_set_finish(self._h, int(pass_), int(max_slots)), "rt_set_finish")
+
+    def set_pipeline(self, depth: int) -> None:
+        """rt_set_pipeline: frames in flight across one-frame calls (1: off; results unchanged)."""
+        self._check(self._L.rt_set_pipeline(self._h, int(depth)), "rt_set_pipeline")
 
     def clear_accum(self) -> None:
         self._check(self._L.rt_clear_accum(self._h), "rt_clear_accum")

@@ -96,6 +96,14 @@ def test_full_size_frames_in_flight_and_history(gpu_renderer, env_maps):
         r.render_async(fp, ro[k:k + 1])
     one_by_one = r.read_accum()
     st_one = r.stats()
+    # one frame per call, pipelined (rt_set_pipeline: calls in flight together)
+    r.clear_accum()
+    r.reset()
+    r.set_pipeline(2)
+    for k in range(n):
+        r.render_async(fp, ro[k:k + 1])
+    pipelined = r.read_accum()
+    r.set_pipeline(1)
     # two calls of 16 frames (progressive history carried in the accumulation buffer)
     r.clear_accum()
     r.reset()
@@ -104,6 +112,7 @@ def test_full_size_frames_in_flight_and_history(gpu_renderer, env_maps):
     halves = r.read_accum()
     assert r.loop_num == n
     assert bit_mismatch(one_by_one, all_at_once)[0] == 0.0
+    assert bit_mismatch(pipelined, all_at_once)[0] == 0.0
     assert bit_mismatch(halves, all_at_once)[0] == 0.0
     assert st_one["rays"] == st_all["rays"]
     assert np.isfinite(all_at_once).mean() > 0.99

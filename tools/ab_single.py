@@ -41,6 +41,8 @@ if a.one is not None:
     r.resize(W, H)
     fp = cf.frame_params(W, H)
     ro = cf.rand_origins(8 + a.calls + 16)
+    if os.environ.get("RT_AB_PIPE"):  # rt_set_pipeline depth (frames in flight across calls)
+        r.set_pipeline(int(os.environ["RT_AB_PIPE"]))
     if os.environ.get("RT_AB_ORDER"):  # rt_order_work from one probe frame before timing
         r.order_work(fp, ro[:1])
     for k in range(8):
