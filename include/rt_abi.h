@@ -222,6 +222,13 @@ int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb);
  * (PNG order).  Synchronous. */
 enum { RT_DISPLAY_TONEMAP = 1, RT_DISPLAY_GAMMA = 2 };
 int rt_tonemap(rt_ctx* ctx, const float* frame_device, int32_t flags, uint8_t* rgb8_host);
+/* The same display pass without waiting for it (main.cpp:228-251: the blit and glfwSwapBuffers
+ * queue the frame and the loop goes on): enqueues the pass and its read-back into internal pinned
+ * slot `slot` (0..3) on the ctx stream, after the render calls queued before it, and returns.  A
+ * render call queued afterwards blends only after this pass has read the accumulation.
+ * rt_display_fetch waits for that slot's image and copies it out (width*height*3 bytes). */
+int rt_tonemap_async(rt_ctx* ctx, const float* frame_device, int32_t flags, int32_t slot);
+int rt_display_fetch(rt_ctx* ctx, int32_t slot, uint8_t* rgb8_host);
 
 #ifdef __cplusplus
 }

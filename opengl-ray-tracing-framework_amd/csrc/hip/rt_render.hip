@@ -120,6 +120,14 @@ struct rt_ctx {
   // leaves idle.  Only the blend waits for the caller's stream (history, frame order); the caller's
   // stream still joins each call at its end.  set_free[p]: the last call on set p has finished;
   // batch_done: the last batched (non-pipelined) call has finished.
+  // rt_tonemap_async: display passes read back into pinned host slots, fetched later
+  static constexpr int DISP_SLOTS = 4;
+  struct DisplaySlot {
+    uint8_t* host = nullptr;
+    size_t cap = 0, bytes = 0;
+    hipEvent_t ev = nullptr;
+  };
+  DisplaySlot disp[DISP_SLOTS];
   int pipe_depth = 1;
   int pipe_next = 0;
   hipEvent_t set_free[MAX_GROUPS] = {};
@@ -510,6 +518,13 @@ int upload(rt_ctx* c, void** dst, const void* src, size_t bytes) {
   return RT_OK;
 }
 
+// Renders in flight read the scene, environment and pixel buffers: an entry point that replaces
+// them first waits for them (the caller's stream joins every render call, pipelined ones too)
+int drain(rt_ctx* c) {
+  if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
 int occupancy(rt_ctx* c) {
   int lds = c->stack_entries * 256 * 8;
   int bpc = 0;
@@ -756,6 +771,10 @@ int rt_destroy(rt_ctx* c) {
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   for (auto& a : c->aux) if (a) (void)hipStreamDestroy(a);
+  for (auto& d : c->disp) {
+    if (d.ev) (void)hipEventDestroy(d.ev);
+    if (d.host) (void)hipHostFree(d.host);
+  }
   for (auto& t : c->ft) {
     if (t.ev) (void)hipEventDestroy(t.ev);
     if (t.h) (void)hipHostFree(t.h);
@@ -792,6 +811,7 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
     return fail(c, RT_ERR_ARG, "missing triangle arrays");
   if (nt >= (1 << 27)) return fail(c, RT_ERR_LIMIT, "more than 2^27 triangles");
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = drain(c)) return rc;
   for (int i = 0; i < nt; i++)
     if (s->material_id[i] < 0 || s->material_id[i] >= s->n_materials)
       return fail(c, RT_ERR_ARG, "material_id out of range");
@@ -951,6 +971,7 @@ int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_materi
   if (!c->scene_set) return fail(c, RT_ERR_STATE, "no scene");
   if ((int64_t)first + count > c->n_tri) return fail(c, RT_ERR_ARG, "range outside the triangle list");
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = drain(c)) return rc;
   float packed[32];
   pack_material(*m, packed);
   int id = -1;
@@ -977,6 +998,7 @@ int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_materi
 int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32_t h, int32_t res) {
   if (!c || !hdr || !cache || w <= 0 || h <= 0) return RT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = drain(c)) return rc;
   // {hdrMap.rgb, hdrCache.b} per texel (a direction's colour and pdf in one fetch) + hdrCache.rg
   std::vector<float4> a((size_t)w * h);
   std::vector<float2> b((size_t)w * h);
@@ -997,8 +1019,7 @@ int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32
 // coherence) and the wavefront state sized for it.
 static int apply_tiling(rt_ctx* c, int width, int height, const rt_tiling& tl, std::vector<int32_t> owner) {
   HIPCHK(c, hipSetDevice(c->device));
-  // renders in flight read the buffers replaced below (the caller's stream joins every call)
-  if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (int rc = drain(c)) return rc;  // renders in flight read the buffers replaced below
   // the old pixel lists / accumulation no longer describe the frame from here on: a failure
   // below leaves the context un-sized (rt_render_async then refuses) rather than half-resized
   c->frame_set = false;
@@ -1692,14 +1713,15 @@ int rt_render(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin, in
   return st ? rt_stats_get(c, st) : rt_synchronize(c);
 }
 
-int rt_tonemap(rt_ctx* c, const float* frame_device, int32_t flags, uint8_t* rgb8_host) {
-  if (!c || !rgb8_host) return RT_ERR_ARG;
+// the display pass into c->d_disp on the ctx stream (after every render call queued before it)
+static int display_kernel(rt_ctx* c, const float* frame_device, int32_t flags) {
   if (!c->frame_set) return fail(c, RT_ERR_STATE, "resize first");
   if (!frame_device && c->world != 1)
     return fail(c, RT_ERR_STATE, "a multi-rank context displays an assembled frame (rt_assemble_frame)");
   HIPCHK(c, hipSetDevice(c->device));
   const size_t bytes = (size_t)c->W * c->H * 3;
   if (bytes > c->disp_bytes) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // an earlier display may still read it
     dfree(c->d_disp);
     HIPCHK(c, hipMalloc(&c->d_disp, bytes));
     c->disp_bytes = bytes;
@@ -1709,8 +1731,44 @@ int rt_tonemap(rt_ctx* c, const float* frame_device, int32_t flags, uint8_t* rgb
                      frame_device ? nullptr : c->d_accum, frame_device, (unsigned char*)c->d_disp, c->W, c->H,
                      c->tile_w, c->tile_h, c->tiles_x, (int)flags);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(rgb8_host, c->d_disp, bytes, hipMemcpyDeviceToHost, c->stream));
+  return RT_OK;
+}
+
+int rt_tonemap(rt_ctx* c, const float* frame_device, int32_t flags, uint8_t* rgb8_host) {
+  if (!c || !rgb8_host) return RT_ERR_ARG;
+  if (int rc = display_kernel(c, frame_device, flags)) return rc;
+  HIPCHK(c, hipMemcpyAsync(rgb8_host, c->d_disp, (size_t)c->W * c->H * 3, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+int rt_tonemap_async(rt_ctx* c, const float* frame_device, int32_t flags, int32_t slot) {
+  if (!c || slot < 0 || slot >= rt_ctx::DISP_SLOTS) return RT_ERR_ARG;
+  rt_ctx::DisplaySlot& d = c->disp[slot];
+  if (d.ev) HIPCHK(c, hipEventSynchronize(d.ev));  // the slot's previous image has been copied out
+  if (int rc = display_kernel(c, frame_device, flags)) return rc;
+  const size_t bytes = (size_t)c->W * c->H * 3;
+  if (bytes > d.cap) {
+    if (d.host) (void)hipHostFree(d.host);
+    d.host = nullptr;
+    d.cap = 0;
+    HIPCHK(c, hipHostMalloc((void**)&d.host, bytes));
+    d.cap = bytes;
+  }
+  if (!d.ev) HIPCHK(c, hipEventCreateWithFlags(&d.ev, hipEventDisableTiming));
+  HIPCHK(c, hipMemcpyAsync(d.host, c->d_disp, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(d.ev, c->stream));
+  d.bytes = bytes;
+  return RT_OK;
+}
+
+int rt_display_fetch(rt_ctx* c, int32_t slot, uint8_t* rgb8_host) {
+  if (!c || !rgb8_host || slot < 0 || slot >= rt_ctx::DISP_SLOTS) return RT_ERR_ARG;
+  rt_ctx::DisplaySlot& d = c->disp[slot];
+  if (!d.ev || !d.bytes) return fail(c, RT_ERR_STATE, "rt_display_fetch: nothing displayed into this slot");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventSynchronize(d.ev));
+  memcpy(rgb8_host, d.host, d.bytes);
   return RT_OK;
 }
 

@@ -141,8 +141,19 @@ class Session:
     """main.cpp's render loop over a Renderer that already holds the scene and environment."""
 
     def __init__(self, renderer: Renderer, width: int, height: int, settings: Optional[Settings] = None,
-                 camera: Optional[Camera] = None, rand_seed: int = cf.RAND_SEED, max_frames: int = 1 << 16):
+                 camera: Optional[Camera] = None, rand_seed: int = cf.RAND_SEED, max_frames: int = 1 << 16,
+                 frames_in_flight: int = 1):
+        """frames_in_flight > 1: the GL driver's frame queue (glfwSwapBuffers does not wait for the
+        frame, main.cpp:251): tick() queues its frame and display pass without waiting
+        (rt_set_pipeline, rt_tonemap_async) and returns the frame displayed frames_in_flight - 1
+        ticks earlier (None while the queue fills; flush() returns the rest).  Images unchanged."""
+        if not 1 <= frames_in_flight <= 3:
+            raise ValueError("frames_in_flight must be 1, 2 or 3")
         self.r = renderer
+        self.in_flight = frames_in_flight
+        self._queued = []  # (tick result, display slot) of frames whose image is not fetched yet
+        if frames_in_flight > 1 or hasattr(renderer, "set_pipeline"):
+            self.r.set_pipeline(frames_in_flight)
         self.settings = settings or Settings()
         self.width, self.height = width, height
         self.camera = camera or Camera(float(f32(width) / f32(height)))
@@ -215,11 +226,36 @@ class Session:
         fp = self.frame_params()
         ro = self._rand[self.frame:self.frame + 1]
         self.frame += 1
-        self.r.render(fp, ro)  # LoopIncrease under maxIterations happens inside (main.cpp:175)
+        # LoopIncrease under maxIterations happens inside (main.cpp:175)
+        if self.in_flight > 1:
+            self.r.render_async(fp, ro)
+        else:
+            self.r.render(fp, ro)
         out = {"params": fp, "loop_num": self.r.loop_num, "rand_origin": float(ro[0]), "delta_time": delta_time}
+        s = self.settings
+        flags = (RT_DISPLAY_TONEMAP if s.enable_tone_mapping else 0) | \
+                (RT_DISPLAY_GAMMA if s.enable_tone_mapping and s.enable_gamma_correction else 0)
+        out["display_flags"] = flags
+        if self.in_flight == 1:
+            if display:
+                out["image"] = self.r.tonemap(flags)
+            return out
+        slot = None
         if display:
-            s = self.settings
-            flags = (RT_DISPLAY_TONEMAP if s.enable_tone_mapping else 0) | \
-                    (RT_DISPLAY_GAMMA if s.enable_tone_mapping and s.enable_gamma_correction else 0)
-            out["image"] = self.r.tonemap(flags)
+            slot = self.frame % 4  # at most 3 queued: a slot is fetched before it is reused
+            self.r.tonemap_async(slot, flags)
+        self._queued.append((out, slot))
+        return self._fetch_oldest() if len(self._queued) >= self.in_flight else None
+
+    def _fetch_oldest(self) -> dict:
+        out, slot = self._queued.pop(0)
+        if slot is not None:
+            out["image"] = self.r.display_fetch(slot)
         return out
+
+    def flush(self) -> list:
+        """The queued frames' results, oldest first (frames_in_flight > 1)."""
+        done = []
+        while self._queued:
+            done.append(self._fetch_oldest())
+        return done

@@ -37,6 +37,7 @@ ABI_SYMBOLS = (
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
     "rt_tile_costs", "rt_set_finish", "rt_order_work", "rt_set_pipeline",
+    "rt_tonemap_async", "rt_display_fetch",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -183,6 +184,8 @@ def _bind(L: C.CDLL) -> C.CDLL:
         L.rt_order_work.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32]
     if hasattr(L, "rt_set_pipeline"):
         L.rt_set_pipeline.argtypes = [vp, C.c_int32]
+        L.rt_tonemap_async.argtypes = [vp, vp, C.c_int32, C.c_int32]
+        L.rt_display_fetch.argtypes = [vp, C.c_int32, C.POINTER(C.c_uint8)]
     L.rt_set_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
@@ -415,4 +418,19 @@ class Renderer:
         out = np.zeros((self.height, self.width, 3), np.uint8)
         self._check(self._L.rt_tonemap(self._h, C.c_void_p(frame_ptr) if frame_ptr else None, int(flags),
                                        out.ctypes.data_as(C.POINTER(C.c_uint8))), "rt_tonemap")
+        return out
+
+    def tonemap_async(self, slot: int, flags: int = RT_DISPLAY_TONEMAP | RT_DISPLAY_GAMMA,
+                      frame_ptr: Optional[int] = None) -> None:
+        """Enqueue the display pass and its read-back into pinned slot `slot` (rt_tonemap_async)."""
+        self._check(self._L.rt_tonemap_async(self._h, C.c_void_p(frame_ptr) if frame_ptr else None, int(flags),
+                                             int(slot)), "rt_tonemap_async")
+        self._disp_shape = {**getattr(self, "_disp_shape", {}), int(slot): (self.height, self.width)}
+
+    def display_fetch(self, slot: int) -> np.ndarray:
+        """Wait for slot `slot`'s display pass and return its 8-bit image (rt_display_fetch)."""
+        h, w = getattr(self, "_disp_shape", {}).get(int(slot), (self.height, self.width))
+        out = np.zeros((h, w, 3), np.uint8)
+        self._check(self._L.rt_display_fetch(self._h, int(slot), out.ctypes.data_as(C.POINTER(C.c_uint8))),
+                    "rt_display_fetch")
         return out

@@ -163,3 +163,51 @@ def test_gpu_session_matches_oracle(gpu_renderer, env_maps):
         flags = (RT_DISPLAY_TONEMAP if st.enable_tone_mapping else 0) | \
                 (RT_DISPLAY_GAMMA if st.enable_tone_mapping and st.enable_gamma_correction else 0)
         assert np.array_equal(out["image"], orc.display(ref, flags)), f"tick {k}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("in_flight", [2, 3])
+def test_gpu_session_frames_in_flight_match_oracle(gpu_renderer, env_maps, in_flight):
+    """Session(frames_in_flight > 1): frames and display passes queued without waiting (the GL
+    frame queue); each displayed image, fetched in_flight - 1 ticks later, equals the oracle's
+    image of its own frame, through camera moves, GUI edits and a material update."""
+    from helpers import oracle_render
+    import oracle as orc
+
+    sc = sl.Scene()
+    for o in cf.CONFIGS["C3"].objects:
+        sc.add_mesh(cf.load_mesh(o.mesh), cf.MATERIALS[o.material], o.rotate, o.translate, o.scale, o.smooth)
+    sc.build_bvh(8)
+
+    def scene_data():
+        tri, nodes = sc.encode()
+        return cf.SceneData("custom", sc.counts(), tri, nodes, sc.export_soa(), sc.nodes(), [])
+
+    sd = scene_data()
+    W, H = 96, 64
+    r = gpu_renderer
+    r.set_scene_soa(sd.soa, sd.nodes)
+    r.set_env(env_maps[0], env_maps[1])
+    s = ia.Session(r, W, H, settings=ia.Settings(max_bounce=4), frames_in_flight=in_flight)
+    script = [ia.Input(), ia.Input(), ia.Input(), ia.Input(keys=["w", "d"]), ia.Input(), ia.Input(),
+              ia.Input(mouse=[(10, 10, True), (25, 4, True)]), ia.Input(),
+              ia.Input(materials=[(0, 50000, cf.MATERIALS["golden"])]), ia.Input(),
+              ia.Input(gui={"enable_tone_mapping": False}), ia.Input()]
+    shown = []
+    for inp in script:
+        out = s.tick(inp, delta_time=0.05)
+        if out is not None:
+            shown.append(out)
+    shown += s.flush()
+    assert len(shown) == len(script)
+    # the oracle replays the frames in order; the material update re-encodes the scene as the
+    # renderer's rt_update_materials does (RefreshTriangleMaterial)
+    accum, sdk = None, sd
+    for k, out in enumerate(shown):
+        if k == 8:
+            sc.set_material(0, 50000, cf.MATERIALS["golden"])
+            sdk = scene_data()
+        frame = cf.oracle_frame_params(out["params"], out["loop_num"], out["rand_origin"])
+        accum, _ = oracle_render(sdk, env_maps, W, H, [frame], accum=accum)
+        assert np.array_equal(out["image"], orc.display(accum, out["display_flags"])), f"tick {k}"
+    s.r.set_pipeline(1)

@@ -28,6 +28,8 @@ ap.add_argument("--frames", type=int, default=30, help="loop passes per script p
 ap.add_argument("--out", default="")
 ap.add_argument("--png", action="store_true", help="write the displayed image of each phase under --out")
 ap.add_argument("--no-display", action="store_true", help="skip the per-frame 8-bit read-back")
+ap.add_argument("--in-flight", type=int, default=1,
+                help="frames in flight (Session frames_in_flight: the GL frame queue; images unchanged)")
 a = ap.parse_args()
 
 cfg = cf.CONFIGS[a.config]
@@ -36,7 +38,7 @@ sd = cf.config_scene(a.config)
 r = Renderer(0)
 r.set_scene_soa(sd.soa, sd.nodes)
 r.set_env(*cf.load_env())
-s = ia.Session(r, W, H)
+s = ia.Session(r, W, H, frames_in_flight=a.in_flight)
 dt = 1.0 / 60.0
 phases = [
     ("still", lambda k: ia.Input()),
@@ -47,12 +49,16 @@ phases = [
     ("still_after", lambda k: ia.Input()),
 ]
 s.tick(delta_time=dt, display=not a.no_display)  # first pass: allocations, code objects
-report = {"config": a.config, "width": W, "height": H, "frames_per_phase": a.frames, "phases": {}}
+s.flush()
+report = {"config": a.config, "width": W, "height": H, "frames_per_phase": a.frames, "frames_in_flight": a.in_flight,
+          "phases": {}}
 for name, make in phases:
     r.synchronize()
     t0 = time.perf_counter()
+    out = None
     for k in range(a.frames):
-        out = s.tick(make(k), delta_time=dt, display=not a.no_display)
+        out = s.tick(make(k), delta_time=dt, display=not a.no_display) or out
+    out = (s.flush() or [out])[-1]  # the phase's last displayed frame (the queue drained)
     r.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.frames
     report["phases"][name] = {"ms_per_frame": round(ms, 3), "fps": round(1e3 / ms, 1), "loop_num": out["loop_num"]}
