@@ -130,6 +130,11 @@ struct rt_ctx {
   DisplaySlot disp[DISP_SLOTS];
   int pipe_depth = 1;
   int pipe_next = 0;
+  // a pipelined call's finisher runs 2 of its 3 resident blocks per CU, leaving room for the next
+  // call's passes: C3 1080p back-to-back 2.33 -> 2.10 ms (1 block: the same; synchronised 3.33 ->
+  // 3.24 ms, 1 block 3.50)
+  int pipe_finish_bpc = 2;
+  int pipe_finish_pass = -1;  // -1: finish_pass
   hipEvent_t set_free[MAX_GROUPS] = {};
   hipEvent_t batch_done = nullptr;
 };
@@ -597,6 +602,13 @@ int occupancy(rt_ctx* c) {
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_finish<true, false>, 256, c->trace_lds);
     // the finisher's lanes index the traversal overflow column: never more than the trace grid
     c->finish_bpc = std::max(1, std::min(e == hipSuccess ? b : 1, std::max(c->trace_bpc, c->trace_bpc0)));
+    if (const char* fe = getenv("RT_FINISH_BPC")) c->finish_bpc = std::max(1, std::min(c->finish_bpc, atoi(fe)));
+    c->pipe_finish_bpc = 2;
+    if (const char* fe = getenv("RT_PIPE_FINISH_BPC")) c->pipe_finish_bpc = std::max(1, atoi(fe));
+    c->pipe_finish_bpc = std::min(c->pipe_finish_bpc, c->finish_bpc);
+    if (getenv("RT_DEBUG"))
+      fprintf(stderr, "[rt] wf_finish: occupancy API %d blocks/CU, using %d (pipelined calls %d)\n", b, c->finish_bpc,
+              c->pipe_finish_bpc);
   }
   const size_t lanes = (size_t)c->n_cus * std::max(c->trace_bpc, c->trace_bpc0) * 256;
   const int entries = std::max(c->stack_entries, c->qstack_entries);
@@ -747,6 +759,7 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = getenv("RT_STAGES")) c->stages = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
   if (const char* e = getenv("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
+  if (const char* e = getenv("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = getenv("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
@@ -1388,13 +1401,14 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         const int nfg = WP.n_frames;
         const int stages = std::max(1, std::min(c->stages, nfg));
         // small groups (one frame per call) end their paths in wf_finish after pass finish_pass-1
+        const int fin_pass = (pipe && c->pipe_finish_pass >= 0) ? c->pipe_finish_pass : c->finish_pass;
         const bool finish = stages == 1 && !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
-                            c->finish_pass >= 1 && c->finish_pass <= last_pass &&
+                            fin_pass >= 1 && fin_pass <= last_pass &&
                             ((fp->flags & RT_FLAG_FINISH) || slots_g[g] <= c->finish_slots);
         for (int pass = 0; pass <= last_pass + stages - 1; pass++) {
           WP.pass = pass;
-          if (finish && pass == c->finish_pass) {
-            const dim3 fgrid((unsigned)(c->n_cus * c->finish_bpc));
+          if (finish && pass == fin_pass) {
+            const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
             static const bool fin_prof = getenv("RT_FINISH_PROF") != nullptr;  // development (RT_FINISH_PROF builds)
             static unsigned long long* d_fin_log = nullptr;                    // never freed
             if (fin_prof) {
