@@ -74,7 +74,10 @@ def parse_args(argv=None):
     ap.add_argument("--single-frames", type=int, default=64,
                     help="frames rendered one per rt_render call after the timed region (ms_per_frame_single)")
     ap.add_argument("--pipeline", type=int, default=2,
-                    help="one-frame calls in flight together for ms_per_frame_single (rt_set_pipeline; 1: off)")
+                    help="render calls in flight together (rt_set_pipeline; 1: off): the one-frame calls of "
+                         "ms_per_frame_single, and the steps at N > 1")
+    ap.add_argument("--pipeline-steps", action="store_true",
+                    help="N = 1: steps in flight too (needs two steps' path state: --frames-per-step <= 256 at 1080p)")
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the interleaved t %% N tile map instead of the cost-balanced one")
@@ -325,6 +328,14 @@ def main(argv=None) -> int:
         full[mine] = torch.from_numpy(r.tile_costs(fp, ro[-1:]).astype(np.int64)).to("cuda")
         dist.all_reduce(full)
         r.set_tile_owners(tiling.balance(full.cpu().numpy(), world))
+    # N > 1: consecutive steps in flight together (rt_set_pipeline: each step's launch on its own
+    # stream and path-state set, only its blend ordered after the previous step and the gather),
+    # so a step's latency-bound last passes overlap the next step's first ones (rank share at N = 8:
+    # 81.5 -> 79.5 ms, tools/rank_sim.py).  One GPU runs a step as two launches (both sets would not
+    # fit), so it keeps its frame groups.
+    pipelined = args.pipeline > 1 and (world > 1 or args.pipeline_steps)
+    if pipelined:
+        r.set_pipeline(args.pipeline)
     ad = r.accum_device()
     # path-state budget: a whole step's frames in flight at once (208 B per pixel-frame: 57 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
@@ -444,6 +455,7 @@ def main(argv=None) -> int:
                    "tile": args.tile, "path_slots_per_rank": path_slots,
                    "parallelism": f"pixel-tiles x{world} + frame-end gather",
                    "tile_assignment": "cost-balanced (rt_tile_costs probe frame)" if balanced else "interleaved t % N",
+                   "steps_in_flight": args.pipeline if pipelined else 1,
                    "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
         "kernel": {"name": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "launches": st["trace_launches"],
                    "render_call_ms": round(launch_ms, 4), "render_calls": st["launches"],

@@ -130,6 +130,7 @@ struct rt_ctx {
   DisplaySlot disp[DISP_SLOTS];
   int pipe_depth = 1;
   int pipe_next = 0;
+  size_t pipe_nomem_slots = SIZE_MAX;  // pipelined batches this large did not fit twice
   // a pipelined call's finisher runs 2 of its 3 resident blocks per CU, leaving room for the next
   // call's passes: C3 1080p back-to-back 2.33 -> 2.10 ms (1 block: the same; synchronised 3.33 ->
   // 3.24 ms, 1 block 3.50)
@@ -1183,10 +1184,33 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   if ((fp->flags & RT_FLAG_MEGAKERNEL) && !fp->enable_bsdf)
     return fail(c, RT_ERR_ARG, "BRDF mode (enable_bsdf = 0) runs on the wavefront path only");
   HIPCHK(c, hipSetDevice(c->device));
+  // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12).
+  int n_trace_pre = 0;
+  for (int k = 0, ln = c->loop_num; k < n_frames; k++) {
+    if (fp->max_iterations == -1 || ln < fp->max_iterations) ln++;
+    if (fp->max_iterations == -1 || ln < fp->max_iterations) n_trace_pre++;
+  }
+  // a pipelined call (rt_set_pipeline): see rt_ctx::pipe_depth.  One-frame calls, and calls of
+  // one batch (at most frames_cap frames) whose whole path state fits in each set.
+  static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
+  const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
+  const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
+  bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && n_trace_pre > 0 &&
+              c->n_valid >= 64 * c->n_groups && !c->tile_cost_on &&
+              (n_trace_pre < c->n_groups ||
+               (n_trace_pre <= c->frames_cap && (size_t)n_trace_pre * nv < c->pipe_nomem_slots));
   if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
-    const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
-    int rc;
-    while (true) {  // a budget larger than free HBM runs fewer frames at a time
+    int rc = RT_ERR_NOMEM;
+    if (pipe && n_trace_pre >= c->n_groups) {  // a pipelined batch: the whole call in one set
+      rc = alloc_wavefront(c, (size_t)n_trace_pre * nv);
+      if (rc == RT_ERR_NOMEM) {  // not both sets: this size runs as frame groups from now on
+        c->pipe_nomem_slots = std::min(c->pipe_nomem_slots, (size_t)n_trace_pre * nv);
+        pipe = false;
+      } else if (rc) {
+        return rc;
+      }
+    }
+    while (rc == RT_ERR_NOMEM) {  // a budget larger than free HBM runs fewer frames at a time
       const int per_group = (std::min(c->frames_cap, (int)n_frames) + c->n_groups - 1) / c->n_groups;
       rc = alloc_wavefront(c, (size_t)per_group * nv);
       if (rc != RT_ERR_NOMEM || per_group <= 1) break;
@@ -1196,17 +1220,6 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     for (int g = 1; g < c->n_groups; g++)
       if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
   }
-  // main.cpp:175: LoopNum++ while below maxIterations; frames at the cap copy history (R12).
-  int n_trace_pre = 0;
-  for (int k = 0, ln = c->loop_num; k < n_frames; k++) {
-    if (fp->max_iterations == -1 || ln < fp->max_iterations) ln++;
-    if (fp->max_iterations == -1 || ln < fp->max_iterations) n_trace_pre++;
-  }
-  // a pipelined one-frame call (rt_set_pipeline): see rt_ctx::pipe_depth
-  static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
-  const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
-  const bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && n_trace_pre > 0 &&
-                    n_trace_pre < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
   const int pset = pipe ? c->pipe_next : 0;
   hipStream_t ps = pipe ? c->aux[1 + pset] : c->stream;  // the stream that runs this call
   hipEvent_t e_entry = nullptr;  // pipelined: the caller's stream at entry (the blend waits for it)

@@ -240,34 +240,36 @@ def test_longest_first_work_order_keeps_the_image(gpu_renderer, env_maps, name):
 
 
 @pytest.mark.parametrize("name,depth", [("C3", 2), ("C4", 3)])
-def test_pipelined_one_frame_calls_match_oracle(gpu_renderer, env_maps, name, depth):
-    """rt_set_pipeline: one-frame calls in flight together (alternating streams, path-state sets,
-    camera and frame tables), a camera that moves between calls, a host read and a batched call in
-    between: the image equals the oracle bit for bit at every read, and so does the ray count."""
+def test_pipelined_calls_match_oracle(gpu_renderer, env_maps, name, depth):
+    """rt_set_pipeline: one-frame calls and one-batch calls in flight together (alternating
+    streams, path-state sets, camera and frame tables), a camera that moves between calls, a host
+    read and a two-batch (unpipelined) call in between: the image equals the oracle bit for bit at
+    every read, and so does the ray count."""
     sd = cf.config_scene(name)
     W, H = 96, 72
-    fps = [cf.frame_params(W, H, position=(0.05 * k, 0.1 * (k % 3), 7.0 - 0.2 * k)) for k in range(7)]
-    ro = cf.rand_origins(7)
-    frames = [cf.oracle_frame_params(fps[k], k + 1, ro[k]) for k in range(3)]
-    frames += [cf.oracle_frame_params(fps[3], k + 1, ro[k]) for k in (3, 4)]
-    frames += [cf.oracle_frame_params(fps[k], k + 1, ro[k]) for k in (5, 6)]
+    fps = [cf.frame_params(W, H, position=(0.05 * k, 0.1 * (k % 3), 7.0 - 0.2 * k)) for k in range(10)]
+    ro = cf.rand_origins(10)
+    # calls: three one-frame, one of 3 frames (two batches of at most 2), one of 2 frames (one
+    # batch: pipelined), two one-frame; each call's frames use its first frame's camera
+    calls = [(0, 1), (1, 1), (2, 1), (3, 3), (6, 2), (8, 1), (9, 1)]
+    frames = [cf.oracle_frame_params(fps[k0], k + 1, ro[k]) for k0, n in calls for k in range(k0, k0 + n)]
     ref3, _ = oracle_render(sd, env_maps, W, H, frames[:3])
     ref, cnt = oracle_render(sd, env_maps, W, H, frames)
     r = gpu_renderer
     r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(*env_maps)
     r.resize(W, H)
+    r.set_max_paths(2 * W * H)  # at most 2 frames per batch
     r.set_pipeline(depth)
     r.order_work(fps[0], cf.rand_origins(1))
     r.reset_stats()
-    for k in range(3):
-        r.render_async(fps[k], ro[k:k + 1])
-    assert bit_mismatch(r.read_accum(), ref3)[0] == 0.0
-    r.render_async(fps[3], ro[3:5])      # a batched call between pipelined ones
-    for k in (5, 6):
-        r.render_async(fps[k], ro[k:k + 1])
+    for i, (k0, n) in enumerate(calls):
+        r.render_async(fps[k0], ro[k0:k0 + n])
+        if i == 2:
+            assert bit_mismatch(r.read_accum(), ref3)[0] == 0.0
     st = r.stats()
-    assert r.loop_num == 7
+    assert r.loop_num == 10
     assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
     assert st["rays"] == cnt["rays"]
     r.set_pipeline(1)
+    r.set_max_paths(0)

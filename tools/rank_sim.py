@@ -28,6 +28,8 @@ ap.add_argument("--reps", type=int, default=1)
 ap.add_argument("--worlds", default="1,2,4,8")
 ap.add_argument("--tile", type=int, default=32)
 ap.add_argument("--out", default=None)
+ap.add_argument("--pipeline", type=int, default=1, help="rt_set_pipeline depth (calls in flight together)")
+ap.add_argument("--calls", type=int, default=1, help="render calls per step (the step's frames split evenly)")
 ap.add_argument("--assign", default="both", choices=["modulo", "balanced", "both"],
                 help="tile owner map: interleaved t %% N, bench.py's cost-balanced map, or both")
 a = ap.parse_args()
@@ -38,6 +40,7 @@ W, H = cfg.width, cfg.height
 fp = cf.frame_params(W, H)
 ro = cf.rand_origins(a.frames + 1)
 r = Renderer(0)
+r.set_pipeline(a.pipeline)
 r.set_scene_soa(sd.soa, sd.nodes)
 r.set_env(*env)
 lines = []
@@ -57,18 +60,21 @@ for world, mode in [(int(x), m) for x in a.worlds.split(",") for m in modes]:
             r.set_tile_owners(owner)
         ad = r.accum_device()
         r.set_max_paths(a.frames * ad["local_tiles"] * a.tile * a.tile)
-        r.render(fp, ro[1:a.frames + 1])          # warm: path-state allocation, first launches
+        per = a.frames // a.calls
+        for c in range(a.calls):                  # warm: path-state allocation, first launches
+            r.render_async(fp, ro[1 + c * per:1 + (c + 1) * per])
         r.synchronize()
         r.reset_stats()
         t = time.perf_counter()
         for _ in range(a.reps):
-            r.render_async(fp, ro[1:a.frames + 1])
+            for c in range(a.calls):
+                r.render_async(fp, ro[1 + c * per:1 + (c + 1) * per])
         r.synchronize()
         times.append((time.perf_counter() - t) / a.reps)
         rays.append(r.stats()["rays"] / a.reps)
     tmax, tmean = max(times), sum(times) / len(times)
     t1 = tmax if t1 is None else t1
-    d = {"config": a.config, "world": world, "assign": mode, "frames": a.frames, "rank_ms": [round(x * 1e3, 1) for x in times],
+    d = {"config": a.config, "world": world, "assign": mode, "frames": a.frames, "pipeline": a.pipeline, "calls": a.calls, "rank_ms": [round(x * 1e3, 1) for x in times],
          "max_ms": round(tmax * 1e3, 1), "mean_ms": round(tmean * 1e3, 1), "imbalance": round(tmax / tmean, 4),
          "mrays_per_s_job": round(sum(rays) / tmax / 1e6, 1), "efficiency_vs_n1": round(t1 / (world * tmax), 4)}
     lines.append(d)
