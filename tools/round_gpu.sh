@@ -17,3 +17,6 @@ cp profiles/${TAG}_* profiles/pmc_C3.json gpurun_out/profiles/
 timeout -k 10 300 python3 tools/interactive_demo.py --config C3 --frames 60 --out gpurun_out/interactive > gpurun_out/interactive.log 2>&1 || { echo "interactive failed"; tail -5 gpurun_out/interactive.log; exit 1; }
 cp gpurun_out/interactive/C3_interactive.json gpurun_out/profiles/${TAG}_interactive.json
 tail -7 gpurun_out/interactive.log
+timeout -k 10 300 python3 tools/interactive_demo.py --config C3 --frames 60 --in-flight 2 --out gpurun_out/interactive2 > gpurun_out/interactive2.log 2>&1 || { echo "interactive (2 in flight) failed"; tail -5 gpurun_out/interactive2.log; exit 1; }
+cp gpurun_out/interactive2/C3_interactive.json gpurun_out/profiles/${TAG}_interactive_in_flight2.json
+tail -7 gpurun_out/interactive2.log
