@@ -166,9 +166,11 @@ int rt_set_max_paths(rt_ctx* ctx, uint64_t slots);
 int rt_set_finish(rt_ctx* ctx, int32_t pass, uint64_t max_slots);
 /* Frames in flight across one-frame calls (the GL driver's own frame queue: main.cpp:175-251
  * issues a draw per loop pass and glfwSwapBuffers does not wait for it to finish).  With depth
- * >= 2, consecutive one-frame rt_render_async calls run on `depth` (at most 3) alternating
- * internal streams with their own path state, so call k+1's early passes overlap call k's
- * latency-bound last bounces.  Only call k+1's blend waits for the ctx stream (call k's blend and
+ * 2 (the most; 1 = off), a one-frame rt_render_async call made while the previous call is
+ * still running runs on the other of two internal streams with its own path state, so call k+1's
+ * early passes overlap call k's latency-bound last bounces (a call with nothing in flight keeps
+ * the lower-latency split into pixel groups).  Calls of one batch are pipelined the same way when
+ * two sets of their path state fit the budget.  Only call k+1's blend waits for the ctx stream (call k's blend and
  * whatever the caller queued there since), and the ctx stream still joins every call at its end:
  * results and ordering are those of depth 1.  Default 1; synchronises the ctx. */
 int rt_set_pipeline(rt_ctx* ctx, int32_t depth);

@@ -114,7 +114,7 @@ struct rt_ctx {
   int finish_pass = 2;  // C3 1080p single frames: 1 / 2 / 3 -> 3.73 / 3.35 / 3.41 ms (off: 3.79)
   uint64_t finish_slots = uint64_t(8) << 20;
   int finish_bpc = 0;              // wf_finish blocks per CU
-  // Pipelined one-frame calls (rt_set_pipeline, depth D >= 2): one-frame call k runs as a single
+  // Pipelined one-frame calls (rt_set_pipeline, depth D = 2): one-frame call k runs as a single
   // group on stream aux[1 + p], p = k mod D, with path-state set wfg[p], camera table p and frame
   // table ft[1 + p], so call k+1's early passes fill the CUs that call k's latency-bound finisher
   // leaves idle.  Only the blend waits for the caller's stream (history, frame order); the caller's
@@ -1164,7 +1164,7 @@ int rt_set_pipeline(rt_ctx* c, int32_t depth) {
   if (!c || depth < 1) return RT_ERR_ARG;
   int rc = rt_synchronize(c);  // calls in flight keep the sets they were given
   if (rc) return rc;
-  c->pipe_depth = std::min<int>(depth, rt_ctx::MAX_GROUPS - 1);  // streams aux[1 ..]
+  c->pipe_depth = std::min<int>(depth, 2);  // streams aux[1], aux[2]
   c->pipe_next = 0;
   return RT_OK;
 }
@@ -1199,6 +1199,15 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               c->n_valid >= 64 * c->n_groups && !c->tile_cost_on &&
               (n_trace_pre < c->n_groups ||
                (n_trace_pre <= c->frames_cap && (size_t)n_trace_pre * nv < c->pipe_nomem_slots));
+  if (pipe && n_trace_pre < c->n_groups && pix_ok) {
+    // a one-frame call with no call in flight has nothing to overlap: the pixel-split groups
+    // (below) have the lower latency (C4 1080p 5.6 vs 6.8 ms synchronised)
+    bool idle = !(c->batch_done && hipEventQuery(c->batch_done) != hipSuccess);
+    for (int q = 0; q < pipe_sets && idle; q++)
+      if (c->set_free[q] && hipEventQuery(c->set_free[q]) != hipSuccess) idle = false;
+    (void)hipGetLastError();  // (hipErrorNotReady is a status, not an error)
+    if (idle) pipe = false;
+  }
   if (!(fp->flags & RT_FLAG_MEGAKERNEL) && n_frames > 0) {
     int rc = RT_ERR_NOMEM;
     if (pipe && n_trace_pre >= c->n_groups) {  // a pipelined batch: the whole call in one set
@@ -1221,7 +1230,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       if (!c->aux[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking));
   }
   const int pset = pipe ? c->pipe_next : 0;
-  hipStream_t ps = pipe ? c->aux[1 + pset] : c->stream;  // the stream that runs this call
+  // the stream that runs this call: pipelined sets on aux[1], aux[2] (aux[1] is also the second
+  // frame group's stream: a pipelined call waits for unpipelined ones anyway, and a fourth stream
+  // measured as losing the overlap, GPU_MAX_HW_QUEUES being 4)
+  hipStream_t ps = pipe ? c->aux[1 + pset] : c->stream;
   hipEvent_t e_entry = nullptr;  // pipelined: the caller's stream at entry (the blend waits for it)
   if (pipe) {
     c->pipe_next = (c->pipe_next + 1) % pipe_sets;
@@ -1705,8 +1717,8 @@ int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   std::stable_sort(sorted.begin(), sorted.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
   // dealt round-robin into the n_groups ranges a one-frame call splits the pixels into, so every
   // group gets an even share of the costly blocks, each in descending order
-  // (a pipelined one-frame call is one range: rt_set_pipeline)
-  const int G = (c->pipe_depth >= 2 && c->n_groups >= 2) ? 1 : std::max(1, c->n_groups);
+  int G = std::max(1, c->n_groups);
+  if (const char* e = getenv("RT_ORDER_RANGES")) G = std::max(1, atoi(e));  // (measurement)
   order.reserve(nb);
   for (int g = 0; g < G; g++)
     for (size_t k = (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);

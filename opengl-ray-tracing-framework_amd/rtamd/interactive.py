@@ -146,7 +146,9 @@ class Session:
         """frames_in_flight > 1: the GL driver's frame queue (glfwSwapBuffers does not wait for the
         frame, main.cpp:251): tick() queues its frame and display pass without waiting
         (rt_set_pipeline, rt_tonemap_async) and returns the frame displayed frames_in_flight - 1
-        ticks earlier (None while the queue fills; flush() returns the rest).  Images unchanged."""
+        ticks earlier (None while the queue fills; flush() returns the rest).  Images unchanged.
+        (The library overlaps at most two render calls; a third queued frame deepens the display
+        queue only.)"""
         if not 1 <= frames_in_flight <= 3:
             raise ValueError("frames_in_flight must be 1, 2 or 3")
         self.r = renderer
