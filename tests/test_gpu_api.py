@@ -273,3 +273,25 @@ def test_pipelined_calls_match_oracle(gpu_renderer, env_maps, name, depth):
     assert st["rays"] == cnt["rays"]
     r.set_pipeline(1)
     r.set_max_paths(0)
+
+
+@pytest.mark.parametrize("n,cap", [(11, 4), (9, 4), (6, 2)])
+def test_batches_of_one_call_match_oracle(gpu_renderer, env_maps, n, cap):
+    """A call of more frames than the path budget holds runs as several batches of frame groups
+    (a last batch of one frame splits by pixels): the image and the ray count equal the oracle's."""
+    sd = cf.config_scene("C3")
+    W, H = 80, 56
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, n)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    r = gpu_renderer
+    r.set_scene_soa(sd.soa, sd.nodes)
+    r.set_env(*env_maps)
+    r.resize(W, H)
+    r.set_max_paths(cap * W * H)
+    r.reset_stats()
+    st = r.render(fp, ro)
+    assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
+    assert st["rays"] == cnt["rays"]
+    assert st["launches"] == (n + cap - 1) // cap
+    r.set_max_paths(0)
