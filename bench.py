@@ -75,9 +75,9 @@ def parse_args(argv=None):
                     help="frames rendered one per rt_render call after the timed region (ms_per_frame_single)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="render calls in flight together (rt_set_pipeline; 1: off): the one-frame calls of "
-                         "ms_per_frame_single, and the steps at N > 1")
+                         "ms_per_frame_single (and the steps with --pipeline-steps)")
     ap.add_argument("--pipeline-steps", action="store_true",
-                    help="N = 1: steps in flight too (needs two steps' path state: --frames-per-step <= 256 at 1080p)")
+                    help="steps in flight together too (two steps' path state: at N = 1 --frames-per-step <= 256 at 1080p)")
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the interleaved t %% N tile map instead of the cost-balanced one")
@@ -328,12 +328,12 @@ def main(argv=None) -> int:
         full[mine] = torch.from_numpy(r.tile_costs(fp, ro[-1:]).astype(np.int64)).to("cuda")
         dist.all_reduce(full)
         r.set_tile_owners(tiling.balance(full.cpu().numpy(), world))
-    # N > 1: consecutive steps in flight together (rt_set_pipeline: each step's launch on its own
-    # stream and path-state set, only its blend ordered after the previous step and the gather),
-    # so a step's latency-bound last passes overlap the next step's first ones (rank share at N = 8:
-    # 81.5 -> 79.5 ms, tools/rank_sim.py).  One GPU runs a step as two launches (both sets would not
-    # fit), so it keeps its frame groups.
-    pipelined = args.pipeline > 1 and (world > 1 or args.pipeline_steps)
+    # --pipeline-steps: consecutive steps in flight together (rt_set_pipeline: each step's launch on
+    # its own stream and path-state set, only its blend ordered after the previous step and the
+    # gather).  Off by default: in steady state (step k+2 waits for step k) a rank's share at N = 8
+    # measured the same (tools/rank_sim.py --pipeline 2, 3 steps: 81.7 vs 81.6 ms), and one GPU runs
+    # a step as two launches whose state fills the HBM once.
+    pipelined = args.pipeline > 1 and args.pipeline_steps
     if pipelined:
         r.set_pipeline(args.pipeline)
     ad = r.accum_device()
