@@ -81,6 +81,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-gather", action="store_true", help="skip the frame-end gather (diagnostics only)")
     ap.add_argument("--no-balance", action="store_true",
                     help="N > 1: keep the interleaved t %% N tile map instead of the cost-balanced one")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 on ONE GPU: every rank on device 0, collectives over gloo on host copies "
+                         "(tests the multi-rank render, balance, gather and assembly without RCCL)")
+    ap.add_argument("--frame-sha", action="store_true",
+                    help="rank 0 adds the sha256 of the assembled fp32 frame after the timed steps")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launcher, frame plan, tiling and the gloo gather only (CPU tests)")
     return ap.parse_args(argv)
@@ -287,10 +292,15 @@ def main(argv=None) -> int:
         return dry_run(args, rank, world)
     import torch
     dist = None
-    torch.cuda.set_device(local_rank)
+    dev = 0 if args.rehearse else local_rank
+    torch.cuda.set_device(dev)
+    cdev = "cpu" if args.rehearse else "cuda"  # where the collectives' tensors live
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if args.rehearse:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
 
     from rtamd import configs as cf
     from rtamd.renderer import RT_FLAG_COUNT_VISITS, Renderer
@@ -310,7 +320,7 @@ def main(argv=None) -> int:
     # finished tiles and the assemble reads the gathered ones.
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    r = Renderer(local_rank)
+    r = Renderer(dev)
     r.set_stream(stream.cuda_stream)
     r.set_scene_soa(sd.soa, sd.nodes)
     r.set_env(*env)
@@ -322,10 +332,10 @@ def main(argv=None) -> int:
         # summed into the full cost vector, and every rank derives the same LPT owner map
         from rtamd import tiling
         n_t = len(tiling.modulo_owners(W, H, args.tile, args.tile, world))
-        full = torch.zeros(n_t, dtype=torch.int64, device="cuda")
+        full = torch.zeros(n_t, dtype=torch.int64, device=cdev)
         mine = torch.tensor(tiling.local_tiles(W, H, args.tile, args.tile, rank, world), dtype=torch.int64,
-                            device="cuda")
-        full[mine] = torch.from_numpy(r.tile_costs(fp, ro[-1:]).astype(np.int64)).to("cuda")
+                            device=cdev)
+        full[mine] = torch.from_numpy(r.tile_costs(fp, ro[-1:]).astype(np.int64)).to(cdev)
         dist.all_reduce(full)
         r.set_tile_owners(tiling.balance(full.cpu().numpy(), world))
     # --pipeline-steps: consecutive steps in flight together (rt_set_pipeline: each step's launch on
@@ -355,8 +365,14 @@ def main(argv=None) -> int:
             r.assemble_frame(ad["ptr"], 1, frame.data_ptr())
             return
         r.copy_accum_device(local.data_ptr(), ad["bytes"])
-        parts = list(gathered.view(world, nfloat).unbind(0)) if rank == 0 else None
-        dist.gather(local, gather_list=parts, dst=0)
+        if args.rehearse:  # gloo: host copies
+            parts = [torch.empty(nfloat, dtype=torch.float32) for _ in range(world)] if rank == 0 else None
+            dist.gather(local.cpu(), gather_list=parts, dst=0)
+            if rank == 0:
+                gathered.copy_(torch.cat(parts))
+        else:
+            parts = list(gathered.view(world, nfloat).unbind(0)) if rank == 0 else None
+            dist.gather(local, gather_list=parts, dst=0)
         if rank == 0:
             r.assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
 
@@ -380,7 +396,7 @@ def main(argv=None) -> int:
     st = r.stats()
 
     # whole-job aggregates
-    vals = torch.tensor([elapsed, float(st["rays"]), float(st["samples"])], dtype=torch.float64, device="cuda")
+    vals = torch.tensor([elapsed, float(st["rays"]), float(st["samples"])], dtype=torch.float64, device=cdev)
     if dist:
         t_max = vals[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -389,6 +405,12 @@ def main(argv=None) -> int:
         elapsed, rays, samples = float(t_max[0]), float(sums[0]), float(sums[1])
     else:
         rays, samples = float(st["rays"]), float(st["samples"])
+
+    frame_sha = None
+    if args.frame_sha and rank == 0 and frame is not None and not args.no_gather:
+        import hashlib
+        torch.cuda.synchronize()
+        frame_sha = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
 
     # the reference's usage pattern (main.cpp:165-200): one frame per draw, outside the timed
     # region; throughput of back-to-back single-frame calls and the latency of a synchronised one
@@ -462,6 +484,10 @@ def main(argv=None) -> int:
                    "trace_share": round(st["trace_ms"] / max(1e-9, st["kernel_ms"]), 4)},
         "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
     }
+    if frame_sha:
+        out["frame_sha256"] = frame_sha
+    if args.rehearse:
+        out["rehearsal"] = "all ranks on one GPU, gloo collectives (not a scaling measurement)"
     if vis["rays"]:
         out["own_traversal_per_ray"] = {"internal": round(vis["internal_pops"] / vis["rays"], 2),
                                         "leaf": round(vis["leaf_pops"] / vis["rays"], 2),
