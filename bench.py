@@ -6,8 +6,8 @@ HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs
 One *step* = ``--frames-per-step`` (default 1024 = the C3 config's spp)
 progressive frames (1 spp each) of the whole frame, rendered by one rt_render call per rank
 over that rank's pixel tiles with as many frames in flight as HBM holds (rt_set_max_paths:
-208 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 229 GB of path
-state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 57 GB per rank),
+192 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 206 GB of path
+state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 51 GB per rank),
 followed by the frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over
 xGMI via torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
 
@@ -347,9 +347,9 @@ def main(argv=None) -> int:
     if pipelined:
         r.set_pipeline(args.pipeline)
     ad = r.accum_device()
-    # path-state budget: a whole step's frames in flight at once (208 B per pixel-frame: 57 GB
+    # path-state budget: a whole step's frames in flight at once (192 B per pixel-frame: 51 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
-    # until the state fits (512 = 229 GB of HBM3E on one GPU)
+    # until the state fits (512 = 206 GB of HBM3E on one GPU)
     path_slots = F * ad["local_tiles"] * args.tile * args.tile
     r.set_max_paths(path_slots)
     nfloat = ad["bytes"] // 4

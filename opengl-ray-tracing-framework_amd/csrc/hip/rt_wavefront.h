@@ -50,10 +50,12 @@ struct WFState {
 #else
   uint4* __restrict__ s5;    // wseed, bounce, flags, frame
 #endif
-  float4* __restrict__ ro;   // continuation ray origin (xyz)
-  float4* __restrict__ rd;   // continuation ray direction
-  float4* __restrict__ so;   // shadow ray origin
-  float4* __restrict__ sd;   // shadow ray direction
+  // rays in 24 B: {o.xyz, d.x} + {d.y, d.z} (continuation ra/rb, shadow sa/sb); 32 B as two
+  // float4 cost the memory-bound shade 16 B of writes and 8 B of reads per path-bounce
+  float4* __restrict__ ra;
+  float2* __restrict__ rb;
+  float4* __restrict__ sa;
+  float2* __restrict__ sb;
   int2* __restrict__ res;    // per path: [2*p + 0] continuation (tri, t bits), [2*p + 1] shadow
   float4* __restrict__ fin;  // per path: final radiance curColor (RT:1549) awaiting the blend
   const unsigned int* __restrict__ pix_xy;   // per work item: px | py << 16
@@ -63,6 +65,11 @@ struct WFState {
   int* active[2];               // active path ids
   unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
 };
+
+RTD void put_ray(float4* a, float2* b, unsigned int p, float ox, float oy, float oz, float dx, float dy, float dz) {
+  a[p] = make_float4(ox, oy, oz, dx);
+  b[p] = make_float2(dy, dz);
+}
 
 struct WFParams {
   KParams K;  // scene, env, camera, frame geometry; K.n_work = valid pixels of this rank
@@ -202,8 +209,7 @@ __global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
       const unsigned int slot = w * nfr + (unsigned)W.gen_f0 + (item - w * nst);
       uint32_t wseed, f;
       const f3 d = camera_ray(P, S, slot, wseed, f);
-      S.ro[slot] = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
-      S.rd[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+      put_ray(S.ra, S.rb, slot, P.pos[0], P.pos[1], P.pos[2], d.x, d.y, d.z);
 #if RT_S5_PACK
       S.s5[slot] = make_uint2(wseed, PF_CONT | PF_CAMERA);
       (void)f;
@@ -790,10 +796,10 @@ void wf_trace(const WFParams W) {
             entry = S.queue[qin][slot];
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
-            const float4 oo = L.anyhit ? S.so[path] : S.ro[path];
-            const float4 dd = L.anyhit ? S.sd[path] : S.rd[path];
-            L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
-            L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+            const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
+            const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
+            L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
+            L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
           }
           tl_start<WIDE>(P, L);
           haveParked = false;
@@ -1084,8 +1090,10 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       rsh = S.res[2 * path + 1];
     }
     const int2 rc0 = S.res[2 * path];
-    const float4 oo0 = camPass ? make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f) : S.ro[path];
-    const float4 dd0 = camPass ? cam_d : S.rd[path];
+    const float4 ra0 = camPass ? make_float4(P.pos[0], P.pos[1], P.pos[2], cam_d.x) : S.ra[path];
+    const float2 rb0 = camPass ? make_float2(cam_d.y, cam_d.z) : S.rb[path];
+    const float4 oo0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
+    const float4 dd0 = make_float4(ra0.w, rb0.x, rb0.y, 0.0f);
     wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
     if (!(flags & PF_CAMERA)) {
       hist = xyz(a0); evp = a0.w;
@@ -1352,12 +1360,10 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
 #endif
     if (qCont) {
-      S.ro[path] = make_float4(contO.x, contO.y, contO.z, 0.0f);
-      S.rd[path] = make_float4(contD.x, contD.y, contD.z, 0.0f);
+      put_ray(S.ra, S.rb, path, contO.x, contO.y, contO.z, contD.x, contD.y, contD.z);
     }
     if (qShadow) {
-      S.so[path] = make_float4(shO.x, shO.y, shO.z, 0.0f);
-      S.sd[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
+      put_ray(S.sa, S.sb, path, shO.x, shO.y, shO.z, shD.x, shD.y, shD.z);
     }
   }
   SHP_MARK(3)
@@ -1549,10 +1555,10 @@ void wf_finish(const WFParams W) {
     FPROF(fp_raymax = max(fp_raymax, fp_ray); fp_ray = 0;)
     contNext = sh && co;
     L.anyhit = sh;
-    const float4 oo = sh ? S.so[path] : S.ro[path];
-    const float4 dd = sh ? S.sd[path] : S.rd[path];
-    L.ox = oo.x; L.oy = oo.y; L.oz = oo.z;
-    L.dx = dd.x; L.dy = dd.y; L.dz = dd.z;
+    const float4 oa = sh ? S.sa[path] : S.ra[path];
+    const float2 ob = sh ? S.sb[path] : S.rb[path];
+    L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
+    L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
     tl_start<WIDE>(P, L);
   };
   while (true) {
