@@ -36,7 +36,8 @@ enum : uint32_t {
   PF_CMED = 2u,        // medium-emissive term pending (RT:1438)
   PF_CONT = 4u,        // a continuation ray is queued (else the path ends after the shadow ray)
   PF_MEDIUM = 8u,      // mediumSampled (RT:1444)
-  PF_CAMERA = 16u      // the queued continuation ray is the camera ray
+  PF_CAMERA = 16u,     // the queued continuation ray is the camera ray
+  PF_ZLO = 32u         // Lo and Le0 are +0 (all bits): s1 not stored, s3 only with a shadow ray
 };
 
 struct WFState {
@@ -668,6 +669,9 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
                            // +0.4% C3, +1.0% C4 (tools/ab_proc.py, 3 rounds)
 #define RT_QUEUE_KIND_SEG 1
 #endif
+#ifndef RT_ZLO  // skip the all-zero Lo/Le0 rows of the path state (PF_ZLO)
+#define RT_ZLO 1
+#endif
 #ifndef RT_ANYHIT_WAVE  // waves whose busy lanes all trace shadow rays skip the closest-hit work:
                         // measured -1.8% (C3) / -1.6% (C4) against the same queues without it (the
                         // per-iteration ballot and scalar branches cost more than the VALU saved)
@@ -1086,8 +1090,16 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     // uniform test), so no load waits for the flags; the flags still decide what is used
     int2 rsh = make_int2(0, 0);
     if (loadPrev) {
-      a0 = S.s0[path]; a1 = S.s1[path]; a2 = S.s2[path]; a3 = S.s3[path];
+      a0 = S.s0[path]; a2 = S.s2[path];
       rsh = S.res[2 * path + 1];
+      // (RT_ZLO) a path whose Lo and Le0 are +0 (every path after a non-emissive camera hit, whose
+      // NEE is still pending) skips the s1 row and, without a shadow ray, the s3 row
+      if (!RT_ZLO || !(a5.z & PF_ZLO)) {
+        a1 = S.s1[path];
+        a3 = S.s3[path];
+      } else if (a5.z & PF_SHADOW) {
+        a3 = S.s3[path];
+      }
     }
     const int2 rc0 = S.res[2 * path];
     const float4 ra0 = camPass ? make_float4(P.pos[0], P.pos[1], P.pos[2], cam_d.x) : S.ra[path];
@@ -1348,10 +1360,13 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   // ------------------------------------------------------------ enqueue rays
   const bool keep = qShadow || qCont;
   if (keep) {
+    const bool zlo = RT_ZLO && (__float_as_uint(Lo.x) | __float_as_uint(Lo.y) | __float_as_uint(Lo.z) |
+                                __float_as_uint(Le0.x) | __float_as_uint(Le0.y) | __float_as_uint(Le0.z)) == 0u;
+    if (zlo) nflags |= PF_ZLO;
     S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
-    S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
+    if (!zlo) S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
     S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
-    S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
+    if (!zlo || qShadow) S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
     if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
     if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
 #if RT_S5_PACK
