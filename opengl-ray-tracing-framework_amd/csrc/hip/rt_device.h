@@ -108,15 +108,18 @@ RTD Mat load_mat(const float4* __restrict__ mats, int id) {
 
 // ------------------------------------------------------------------ env textures (R13)
 // texture() with NEAREST + CLAMP_TO_EDGE on W x H float4 texels.
-template <class T>
-RTD T tex_nearest(const T* __restrict__ img, int w, int h, float u, float v) {
+RTD unsigned int tex_index(int w, int h, float u, float v) {
   int i = (int)floor_(u * (float)w);
   int j = (int)floor_(v * (float)h);
   if (isnan_(u)) i = 0;
   if (isnan_(v)) j = 0;
   i = i < 0 ? 0 : (i > w - 1 ? w - 1 : i);
   j = j < 0 ? 0 : (j > h - 1 ? h - 1 : j);
-  return img[(size_t)j * w + i];
+  return (unsigned int)j * (unsigned int)w + (unsigned int)i;
+}
+template <class T>
+RTD T tex_nearest(const T* __restrict__ img, int w, int h, float u, float v) {
+  return img[tex_index(w, h, u, v)];
 }
 
 // hdr texel = {hdrMap.rgb, hdrCache.b (pdf)}: hdrColor and hdrPdf of a direction read the same
@@ -125,6 +128,7 @@ RTD T tex_nearest(const T* __restrict__ img, int w, int h, float u, float v) {
 struct Env {
   const float4* __restrict__ hdr;
   const float2* __restrict__ cache;
+  const float4* __restrict__ light;  // per cache texel: {L, hdrPdf(L)}, {hdrColor(L), 0} (rt_light_table_kernel)
   int w, h, res;
   float angle, intensity;
 };
@@ -139,8 +143,7 @@ RTD void toSphericalCoord(const Env& E, f3 v, float& u, float& w) {  // RT:625-6
   u = ux + E.angle;
   w = uy + 0.0f;
 }
-RTD f3 SampleHdr(const Env& E, float xi_1, float xi_2) {  // RT:635-646
-  float2 c = tex_nearest(E.cache, E.w, E.h, xi_1, xi_2);
+RTD f3 SampleHdrTexel(float2 c) {  // RT:637-645: the direction of one hdrCache texel
   float x = c.x;
   float y = 1.0f - c.y;
   float phi = 2.0f * PI * (x - 0.5f);
@@ -149,6 +152,9 @@ RTD f3 SampleHdr(const Env& E, float xi_1, float xi_2) {  // RT:635-646
   sincos_(theta, &st, &ct);
   sincos_(phi, &sp, &cp);
   return mk3(ct * cp, st, ct * sp);
+}
+RTD f3 SampleHdr(const Env& E, float xi_1, float xi_2) {  // RT:635-646
+  return SampleHdrTexel(tex_nearest(E.cache, E.w, E.h, xi_1, xi_2));
 }
 RTD f3 hdrColor(const Env& E, f3 L) {  // RT:1165-1169
   float u, v;
@@ -175,6 +181,18 @@ RTD void hdrColorPdf(const Env& E, f3 L, f3& color, float& pdfv) {
   float sin_theta = max_(sin_(theta), 1e-10f);
   float p_convert = (float)(E.res * E.res / 2) / (TWO_PI * PI * sin_theta);
   pdfv = pdf * p_convert;
+}
+// The NEE light sample of RT:1382-1392 from the per-texel table: SampleHdr(xi_1, xi_2) and
+// hdrColor / hdrPdf of that direction depend only on the hdrCache texel the sample lands on, so
+// rt_light_table_kernel evaluates them once per texel with the same functions (same bits) and a
+// sample costs one 32-B fetch instead of a texel fetch, two sincos, atan2, asin, sin and a
+// second, dependent texel fetch
+RTD void SampleHdrLight(const Env& E, float xi_1, float xi_2, f3& L, f3& color, float& pdf) {
+  const float4* t = E.light + 2u * (size_t)tex_index(E.w, E.h, xi_1, xi_2);
+  const float4 a = t[0], b = t[1];
+  L = xyz(a);
+  pdf = a.w;
+  color = xyz(b);
 }
 RTD f3 getDefaultSkyColor(float y) {  // RT:1190-1193
   float t = 0.5f * (y + 1.0f);

@@ -55,6 +55,7 @@ struct KParams {
   const float4* __restrict__ mats;  // 8 per material
   const float4* __restrict__ hdr;
   const float2* __restrict__ cache;  // hdrCache.rg (hdr.w holds hdrCache.b)
+  const float4* __restrict__ light;  // NEE light samples per hdrCache texel (SampleHdrLight)
   int hdr_w, hdr_h, hdr_res;
   float4* __restrict__ accum;
   unsigned int* __restrict__ counter;
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void rt_path_kernel(const KParams P) {
   const int stride = blockDim.x;
   int* sref = reinterpret_cast<int*>(smem) + threadIdx.x;
   float* sdist = reinterpret_cast<float*>(smem + (size_t)P.stack_entries * stride * 4) + threadIdx.x;
-  const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+  const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
   const int lane = (int)(threadIdx.x & 63);
   const f3 camPos = mk3(P.pos[0], P.pos[1], P.pos[2]);
@@ -473,6 +474,21 @@ RTD f3 simple_aces(f3 c) {  // TM:66-75
   return mk3(clamp_(r.x, 0.0f, 1.0f), clamp_(r.y, 0.0f, 1.0f), clamp_(r.z, 0.0f, 1.0f));
 }
 RTD unsigned char unorm8(float f) { return (unsigned char)(int)(clamp_(f, 0.0f, 1.0f) * 255.0f + 0.5f); }
+
+// NEE light samples per hdrCache texel (SampleHdrLight): the direction SampleHdr returns for the
+// texel, and hdrColor / hdrPdf of that direction (hdrColorPdf) — the same device functions the
+// shade would call, so the same bits.  Depends on envAngle: rebuilt when a call's angle changes.
+__global__ __launch_bounds__(256) void rt_light_table_kernel(const Env E, float4* __restrict__ out) {
+  const unsigned int n = (unsigned int)E.w * (unsigned int)E.h;
+  for (unsigned int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const f3 L = SampleHdrTexel(E.cache[k]);
+    f3 color;
+    float pdf;
+    hdrColorPdf(E, L, color, pdf);
+    out[2u * k] = make_float4(L.x, L.y, L.z, pdf);
+    out[2u * k + 1u] = make_float4(color.x, color.y, color.z, 0.0f);
+  }
+}
 
 __global__ __launch_bounds__(256) void rt_display_kernel(const float4* __restrict__ tiles, const float* __restrict__ frame,
                                                          unsigned char* __restrict__ out, int W, int H, int tile_w,

@@ -45,6 +45,9 @@ struct rt_ctx {
   // env
   float4* d_hdr = nullptr;
   float2* d_cache = nullptr;                  // hdrCache.rg; d_hdr = {hdrMap.rgb, hdrCache.b}
+  float4* d_light = nullptr;                  // NEE light samples per hdrCache texel (rt_light_table_kernel)
+  bool light_valid = false;
+  float light_angle = 0.0f;                   // the envAngle d_light was built for
   int hdr_w = 0, hdr_h = 0, hdr_res = 0;
   bool env_set = false;
   // frame
@@ -780,7 +783,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
-  dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
+  dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_light); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
@@ -1023,6 +1026,9 @@ int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32
   int rc;
   if ((rc = upload(c, (void**)&c->d_hdr, a.data(), a.size() * sizeof(float4)))) return rc;
   if ((rc = upload(c, (void**)&c->d_cache, b.data(), b.size() * sizeof(float2)))) return rc;
+  dfree(c->d_light);
+  HIPCHK(c, hipMalloc(&c->d_light, a.size() * 2 * sizeof(float4)));
+  c->light_valid = false;
   c->hdr_w = w; c->hdr_h = h; c->hdr_res = res;
   c->env_set = true;
   return RT_OK;
@@ -1291,6 +1297,21 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, d_loop, d_sobol, n_traced);
     HIPCHK(c, hipGetLastError());
   }
+  // NEE light table for this call's envAngle (SampleHdrLight); built with nothing in flight, since
+  // pipelined calls do not wait for the ctx stream
+  if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL) &&
+      (!c->light_valid || __builtin_memcmp(&c->light_angle, &fp->env_angle, sizeof(float)) != 0)) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto& a : c->aux) if (a) HIPCHK(c, hipStreamSynchronize(a));
+    const rtd::Env E{c->d_hdr, c->d_cache, c->d_light, c->hdr_w, c->hdr_h, c->hdr_res, fp->env_angle, fp->env_intensity};
+    const unsigned int n = (unsigned int)(c->hdr_w * c->hdr_h);
+    hipLaunchKernelGGL(rtd::rt_light_table_kernel, dim3(std::max(1u, std::min(4096u, (n + 255) / 256))), dim3(256), 0,
+                       c->stream, E, c->d_light);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->light_angle = fp->env_angle;
+    c->light_valid = true;
+  }
   int done = 0;
   while (done < n_traced) {
     KParams P;
@@ -1326,7 +1347,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       P.cull_eps = (eps * sc < 1e30) ? (float)(eps * sc) : INFINITY;
     }
     P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
-    P.hdr = c->d_hdr; P.cache = c->d_cache; P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
+    P.hdr = c->d_hdr; P.cache = c->d_cache; P.light = c->d_light;
+    P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
     if (P.n_work == 0) continue;
     const bool count = (fp->flags & RT_FLAG_COUNT_VISITS) != 0;

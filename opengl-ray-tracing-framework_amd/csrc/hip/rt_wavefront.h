@@ -1214,13 +1214,12 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     const f3 V = -hV, N = hN;
     const float xa = rand_(wseed);
     const float xb = rand_(wseed);
-    const f3 Ll = SampleHdr(E, xa, xb);
+    f3 Ll, light_fr;
+    float light_pdf;
+    SampleHdrLight(E, xa, xb, Ll, light_fr, light_pdf);  // SampleHdr + hdrColorPdf (same bits)
     f3 T, Bt;
     getTangent(N, T, Bt);
     if (dot(N, Ll) > 0.0f) {
-      f3 light_fr;
-      float light_pdf;
-      hdrColorPdf(E, Ll, light_fr, light_pdf);
       light_fr = light_fr * E.intensity;
       float brdf_pdf;
       const f3 brdf_fr = BRDF_Evaluate(V, N, Ll, T, Bt, m, brdf_pdf);
@@ -1272,11 +1271,10 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
     const float xa = rand_(wseed);  // R24
     const float xb = rand_(wseed);
-    const f3 Ll = SampleHdr(E, xa, xb);
+    f3 Ll, light_fr;
+    float light_pdf;
+    SampleHdrLight(E, xa, xb, Ll, light_fr, light_pdf);  // SampleHdr + hdrColorPdf (same bits)
     if (dot(hN, Ll) > 0.0f) {
-      f3 light_fr;
-      float light_pdf;
-      hdrColorPdf(E, Ll, light_fr, light_pdf);
       light_fr = light_fr * E.intensity;
       float disney_eval_pdf;
       const f3 disney_eval_fr = DisneyEval(BF, m, hN, Ll, disney_eval_pdf);
@@ -1400,7 +1398,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const unsigned int na = W.cam_n ? W.cam_n : S.cnt[2 + in];
   const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
   if (blockIdx.x == 0 && threadIdx.x == 0) S.cnt[4] = 0u;  // fetch counter of the next trace pass
-  const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+  const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
   SHP_DECL
@@ -1542,7 +1540,7 @@ void wf_finish(const WFParams W) {
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
-  const Env E{P.hdr, P.cache, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+  const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   TraceStack TS;
   TS.KL = P.lds_entries;
   TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
