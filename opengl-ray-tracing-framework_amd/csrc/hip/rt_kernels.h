@@ -36,6 +36,7 @@ struct KParams {
   const int* __restrict__ loop_num;       // per frame of this launch (device table)
   const float* __restrict__ rand_origin;  // per frame of this launch (device table)
   const float2* __restrict__ sobol;       // per frame of this launch: sobolVec2 of bounces 0..3 (wf_sobol)
+  const float2* __restrict__ blend_w;     // per frame of this launch: blend weights {1/n, (n-1)/n} (wf_sobol)
   int W, H, tile_w, tile_h, tiles_x, rank, world;
   const int* __restrict__ tile_ids;   // global tile id of each local tile (rt_set_tile_owners)
   unsigned long long* __restrict__ tile_cost;  // rt_tile_costs probe: per local tile (else null)

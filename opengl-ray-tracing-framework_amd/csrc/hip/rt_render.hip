@@ -1271,8 +1271,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     dfree(T.d);
     const size_t cap = std::max<size_t>(pipe ? 16 : 1024, (size_t)n_frames);
     HIPCHK(c, hipHostMalloc((void**)&T.h, 2 * cap * sizeof(int)));
-    // device table: [cap] loop_num, [cap] rand_origin, then [cap][4] float2 Sobol pairs (wf_sobol)
-    HIPCHK(c, hipMalloc((void**)&T.d, 10 * cap * sizeof(int)));
+    // device table: [cap] loop_num, [cap] rand_origin, then [cap][4] float2 Sobol pairs and [cap]
+    // float2 blend weights (wf_sobol)
+    HIPCHK(c, hipMalloc((void**)&T.d, 12 * cap * sizeof(int)));
     T.cap = cap;
   }
   if (!T.ev) HIPCHK(c, hipEventCreateWithFlags(&T.ev, hipEventDisableTiming));
@@ -1293,8 +1294,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   const int* d_loop = T.d;
   const float* d_ro = reinterpret_cast<const float*>(T.d + T.cap);
   float2* d_sobol = reinterpret_cast<float2*>(T.d + 2 * T.cap);
+  float2* d_blendw = reinterpret_cast<float2*>(T.d + 10 * T.cap);
   if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
-    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, d_loop, d_sobol, n_traced);
+    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, d_loop, d_sobol, d_blendw,
+                       n_traced);
     HIPCHK(c, hipGetLastError());
   }
   // NEE light table for this call's envAngle (SampleHdrLight); built with nothing in flight, since
@@ -1321,6 +1324,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.loop_num = d_loop + done;
     P.rand_origin = d_ro + done;
     P.sobol = d_sobol + 4 * (size_t)done;
+    P.blend_w = d_blendw + done;
     done += nf;
     memcpy(P.pos, fp->position, 12); memcpy(P.lbc, fp->left_bottom_corner, 12);
     memcpy(P.right, fp->right, 12); memcpy(P.up, fp->up, 12);
@@ -1395,6 +1399,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K.loop_num = P.loop_num + f0;
         WP.K.rand_origin = P.rand_origin + f0;
         WP.K.sobol = P.sobol + 4 * f0;
+        WP.K.blend_w = P.blend_w + f0;
         WP.K.n_frames = f1 - f0;
         WP.K.n_work = w1 - w0;
         WP.K.lds_entries = c->trace_lds_entries;

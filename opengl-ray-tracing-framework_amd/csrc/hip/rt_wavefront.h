@@ -151,8 +151,16 @@ __global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
 #endif
 // Per frame of a render call: sobolVec2(loopNum + 1, bounce) of RT:616-620 for bounces 0..3
 // (Sobol dims 0..7), so wf_shade reads one float2 instead of running two bit loops per bounce.
-__global__ __launch_bounds__(256) void wf_sobol(const int* __restrict__ loop_num, float2* __restrict__ out, int n_frames) {
+// Also the blend weights of each frame, {1 / n, (n - 1) / n} with n = loopNum (RT:1552), the same
+// operations wf_blend would run per pixel.
+__global__ __launch_bounds__(256) void wf_sobol(const int* __restrict__ loop_num, float2* __restrict__ out,
+                                                float2* __restrict__ blend_w, int n_frames) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_frames) {
+    const int loopNum = loop_num[i];
+    const float n = (float)loopNum;
+    blend_w[i] = make_float2(1.0f / n, (float)(loopNum - 1) / n);
+  }
   if (i >= n_frames * 4) return;
   int g = loop_num[i >> 2] + 1;
   g = g ^ (g >> 1);  // grayCode (RT:598-600)
@@ -252,9 +260,8 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
       if (valid)
         for (unsigned int k = 0; k < nfc; k++) {
           const float4 c = tile[threadIdx.x * BL_PITCH + k];
-          const int loopNum = P.loop_num[f0 + k];
-          const float n = (float)loopNum;
-          acc = (1.0f / n) * xyz(c) + ((float)(loopNum - 1) / n) * acc;
+          const float2 bw = P.blend_w[f0 + k];  // {1 / n, (n - 1) / n} (wf_sobol)
+          acc = bw.x * xyz(c) + bw.y * acc;
         }
     }
     if (valid) P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
