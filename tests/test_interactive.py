@@ -104,6 +104,45 @@ class FakeRenderer:
         return np.zeros((1, 1, 3), np.uint8)
 
 
+class FakeAsyncRenderer(FakeRenderer):
+    """FakeRenderer plus the queued display of Session(frames_in_flight > 1)."""
+
+    def __init__(self):
+        super().__init__()
+        self.slots, self.depth = {}, None
+
+    def set_pipeline(self, depth):
+        self.depth = depth
+
+    def render_async(self, fp, ro):
+        self.render(fp, ro)
+
+    def tonemap_async(self, slot, flags):
+        assert slot not in self.slots, "display slot reused before it was fetched"
+        self.slots[slot] = (self.loop, flags)
+
+    def display_fetch(self, slot):
+        loop, flags = self.slots.pop(slot)
+        return np.full((1, 1, 3), loop, np.uint8)
+
+
+def test_session_frames_in_flight_returns_frames_in_order():
+    """Session(frames_in_flight=D): tick k returns frame k-D+1 with its own image (the display
+    queue), None while the queue fills, flush() the rest; slots never reused while queued."""
+    for depth in (2, 3):
+        r = FakeAsyncRenderer()
+        s = ia.Session(r, 16, 16, frames_in_flight=depth)
+        assert r.depth == depth
+        got = [s.tick(delta_time=0.0) for _ in range(7)]
+        assert got[:depth - 1] == [None] * (depth - 1)
+        shown = [g for g in got if g is not None] + s.flush()
+        assert [o["loop_num"] for o in shown] == list(range(1, 8))
+        assert all(int(o["image"][0, 0, 0]) == o["loop_num"] for o in shown)
+        assert not r.slots
+    with pytest.raises(ValueError):
+        ia.Session(FakeAsyncRenderer(), 16, 16, frames_in_flight=4)
+
+
 def test_session_loop_resets_and_rand_stream():
     r = FakeRenderer()
     s = ia.Session(r, 64, 32)
