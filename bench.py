@@ -30,6 +30,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -88,6 +89,8 @@ def parse_args(argv=None):
                     help="rank 0 adds the sha256 of the assembled fp32 frame after the timed steps")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launcher, frame plan, tiling and the gloo gather only (CPU tests)")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="(with --dry-run) this rank exits with status 3 before the rendezvous (launcher test)")
     return ap.parse_args(argv)
 
 
@@ -107,20 +110,44 @@ def launch_ranks(n: int, argv) -> int:
     in it before the children start."""
     port = _free_port()
     procs = []
+    out0 = tempfile.TemporaryFile(mode="w+")  # rank 0's stdout (a file: no pipe to drain while polling)
     for r in range(n):
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
-    out0 = procs[0].communicate()[0] if procs else ""
-    rcs = [p.wait() for p in procs]
-    line = next((ln for ln in reversed(out0.splitlines()) if ln.startswith("{")), None)
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL, text=True))
+    # fail fast: a rank that dies leaves the others blocked in a collective (or the rendezvous)
+    # until its timeout, so the first non-zero exit stops the ranks still running
+    rcs = [None] * n
+    first_fail = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] and first_fail is None:
+                    first_fail = rcs[i]
+        if first_fail is not None:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.2)
+    out0.seek(0)
+    line = next((ln for ln in reversed(out0.read().splitlines()) if ln.startswith("{")), None)
+    out0.close()
     if any(rcs) or line is None:
         print(f"bench.py: rank exit codes {rcs}" + ("" if line else "; rank 0 printed no JSON line"),
               file=sys.stderr)
-        return next((rc for rc in rcs if rc), 1)
+        return first_fail or next((rc for rc in rcs if rc), 1)
     print(line, flush=True)
     return 0
 
@@ -234,6 +261,9 @@ def dry_run(args, rank: int, world: int) -> int:
     W, H = args.width or cfg.width, args.height or cfg.height
     F, steps, warm = args.frames_per_step, args.steps, args.warmup
     total_frames = (warm + steps) * F + 1 + args.single_frames
+    if rank == args.fail_rank:
+        print(f"bench.py: rank {rank} fails on purpose (--fail-rank)", file=sys.stderr)
+        return 3
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     ro = cf.rand_origins(total_frames)

@@ -6,6 +6,7 @@ import ctypes.util
 import json
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -69,3 +70,14 @@ def test_bench_self_launches_two_gloo_ranks():
     d = _bench("--gpus", "2", "--steps", "20", "--warmup", "5", "--dry-run")
     assert d["n_gpus"] == 2 and d["gather_ok"]
     assert d["pixels_covered"] == 1920 * 1080
+
+
+def test_bench_launcher_stops_the_other_ranks_when_one_fails():
+    """A rank that exits early would leave the others waiting in the rendezvous; the launcher
+    stops them and returns the failing rank's status instead of hanging."""
+    t0 = time.time()
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run", "--fail-rank", "1"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert not any(ln.startswith("{") for ln in p.stdout.splitlines())
+    assert time.time() - t0 < 90
