@@ -26,6 +26,16 @@ map's, `rts_hdr_cache`); the object is the reference's bunny mesh in front of th
 The GPU tests also require the HIP image to equal the oracle's bit for bit, and repeat the
 furnace at 1920x1080 (a size-independent property, no oracle).
 
+The plane tests go one step further and pin the *value* of the reference's estimator, not just
+a bound: for a flat floor of F = 1 metal in the furnace every path ends after one bounce, so the
+expected pixel value is a 2-D integral over the hemisphere that numpy evaluates from the BSDF's
+formulas alone (GGX D, separable Smith G1 with alpha = roughness^2, RT:447-471; the VNDF pdf
+G1(V) D / (4 V.z), RT:962; hdrPdf of a constant map 1 / (2 pi^2 sin theta), RT:1173-1186; the
+power-heuristic MIS of RT:1285-1288 on both estimators; the double weight above).  No sampling
+routine enters the integral, so SampleGGXVNDF, SampleHdr, the Sobol/Cranley-Patterson numbers
+and the wavefront bookkeeping are all checked against it: the mean over the floor's pixels must
+equal the integral within the sampling error.
+
 Not covered, by the reference's own design: a dielectric (RT:1429 skips f/pdf on refraction,
 R9) and the Disney diffuse lobe (retro-reflection, albedo != 1) are not energy conserving, and
 with MIS off the light sample and the BSDF sample both count the environment (RT:1396, :1431),
@@ -135,3 +145,84 @@ def test_gpu_white_furnace_full_hd(gpu_renderer, roughness):
     img, st = gpu_render(gpu_renderer, sd, env, W, H, fp, ro)
     assert st["rays"] >= W * H * 16
     check_furnace(img, roughness)
+
+
+# ------------------------------------------------------------------ plane: the estimator's value
+FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scene.h:116-120): y = const
+
+
+def estimator_expectation(mu: float, roughness: float, nth: int = 400, nph: int = 800) -> float:
+    """E[Lo] / (Le * envIntensity) of the reference's BSDF integrator for one bounce off an F = 1
+    metal plane (normal = +y = the env map's pole axis) viewed at cosine mu, constant environment:
+    the light sample (RT:1380-1405) contributes w_l f cos, the escaping BSDF sample (RT:1431,
+    RT:1496) p_b w_b (f cos / p_b)^2, both over the upper hemisphere (midpoint rule)."""
+    a = max(1e-3, roughness * roughness)                       # m.ax = m.ay (RT:205-207)
+    th = (np.arange(nth) + 0.5) * (np.pi / 2) / nth
+    ph = (np.arange(nph) + 0.5) * (2 * np.pi) / nph
+    T, P = np.meshgrid(th, ph, indexing="ij")
+    dw = np.sin(T) * (np.pi / 2 / nth) * (2 * np.pi / nph)
+    L = np.stack([np.sin(T) * np.cos(P), np.sin(T) * np.sin(P), np.cos(T)], -1)
+    V = np.array([np.sqrt(max(0.0, 1 - mu * mu)), 0.0, mu])
+    Hh = L + V
+    Hh /= np.linalg.norm(Hh, axis=-1, keepdims=True)
+    D = 1.0 / (np.pi * a * a * ((Hh[..., 0] / a) ** 2 + (Hh[..., 1] / a) ** 2 + Hh[..., 2] ** 2) ** 2)
+
+    def G1(w):
+        return 2 * w[..., 2] / (w[..., 2] + np.sqrt(a * a * (w[..., 0] ** 2 + w[..., 1] ** 2) + w[..., 2] ** 2))
+
+    g1v, g1l = G1(V), G1(L)
+    fcos = D * g1v * g1l / (4 * mu)       # F D G2 / (4 L.z V.z) * L.z, F = 1
+    pb = g1v * D / (4 * mu)               # VNDF pdf of the reflected direction
+    pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
+    wl = pl ** 2 / (pl ** 2 + pb ** 2)
+    return float(np.sum((wl * fcos + (1 - wl) * pb * g1l ** 2) * dw))
+
+
+def view_cosines(fp, W, H):
+    """cos(angle between the floor normal +y and -ray) of every pixel's camera ray (RT:1520-1527),
+    rows bottom-up as the accumulation buffer stores them."""
+    lbc, right, up = (np.asarray(x, np.float64) for x in (fp.left_bottom_corner, fp.right, fp.up))
+    u = (np.arange(W) + 0.5) / W
+    v = (np.arange(H) + 0.5) / H
+    d = (lbc[None, None, :] + (u[None, :, None] * 2 * fp.half_w) * right[None, None, :]
+         + (v[:, None, None] * 2 * fp.half_h) * up[None, None, :])
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    return -d[..., 1]
+
+
+def check_plane(img, fp, W, H, roughness, rel_tol):
+    v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
+    mu = view_cosines(fp, W, H)
+    on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
+    assert on.sum() > 0.2 * W * H, on.sum()
+    grid = np.linspace(0.02, 1.0, 80)
+    e = np.interp(mu[on], grid, [estimator_expectation(m, roughness) for m in grid])
+    got, want = v[on].mean(), e.mean()
+    se = v[on].std() / np.sqrt(on.sum())
+    assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
+    return got / want
+
+
+def floor_scene(roughness: float):
+    mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=1.0, roughness=roughness, specular=1.0)
+    return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
+
+
+@pytest.mark.parametrize("roughness", [0.5, 0.8])
+def test_oracle_plane_furnace_equals_estimator_integral(roughness):
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    _, frames = frames_for(fp, 1, 64)
+    img, _ = oracle_render(floor_scene(roughness), furnace_env(), W, H, frames)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.002)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("roughness", [0.5, 0.8])
+def test_gpu_plane_furnace_full_hd_equals_estimator_integral(gpu_renderer, roughness):
+    """1920x1080, 8 frames on the GPU against the integral (no oracle): sampling error ~1e-4."""
+    W, H = 1920, 1080
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    ro, _ = frames_for(fp, 1, 8)
+    img, _ = gpu_render(gpu_renderer, floor_scene(roughness), furnace_env(), W, H, fp, ro)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.002)
