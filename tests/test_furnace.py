@@ -151,11 +151,13 @@ def test_gpu_white_furnace_full_hd(gpu_renderer, roughness):
 FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scene.h:116-120): y = const
 
 
-def estimator_expectation(mu: float, roughness: float, nth: int = 400, nph: int = 800) -> float:
-    """E[Lo] / (Le * envIntensity) of the reference's BSDF integrator for one bounce off an F = 1
-    metal plane (normal = +y = the env map's pole axis) viewed at cosine mu, constant environment:
-    the light sample (RT:1380-1405) contributes w_l f cos, the escaping BSDF sample (RT:1431,
-    RT:1496) p_b w_b (f cos / p_b)^2, both over the upper hemisphere (midpoint rule)."""
+def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800):
+    """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
+    (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
+    (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
+    cancels); B = the escaping BSDF sample with its MIS weight, p_b w_b (f cos / p_b)^2 (RT:1431,
+    RT:1496); S[c] = the same sample in sky mode, p_b (f cos / p_b)^2 getDefaultSkyColor(L.y)[c]
+    (RT:1500-1503: no MIS weight, no envIntensity; RT:1190-1193)."""
     a = max(1e-3, roughness * roughness)                       # m.ax = m.ay (RT:205-207)
     th = (np.arange(nth) + 0.5) * (np.pi / 2) / nth
     ph = (np.arange(nph) + 0.5) * (2 * np.pi) / nph
@@ -175,7 +177,18 @@ def estimator_expectation(mu: float, roughness: float, nth: int = 400, nph: int 
     pb = g1v * D / (4 * mu)               # VNDF pdf of the reflected direction
     pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
     wl = pl ** 2 / (pl ** 2 + pb ** 2)
-    return float(np.sum((wl * fcos + (1 - wl) * pb * g1l ** 2) * dw))
+    t = 0.5 * (np.cos(T) + 1.0)
+    sky = [(1 - t) + t * c for c in (0.5, 0.7, 1.0)]
+    A = float(np.sum(wl * fcos * dw))
+    B = float(np.sum((1 - wl) * pb * g1l ** 2 * dw))
+    S = np.array([np.sum(pb * g1l ** 2 * sc * dw) for sc in sky])
+    return A, B, S
+
+
+def estimator_expectation(mu: float, roughness: float) -> float:
+    """Environment mode, relative to Le * envIntensity: A + B."""
+    A, B, _ = estimator_terms(mu, roughness)
+    return A + B
 
 
 def view_cosines(fp, W, H):
@@ -226,3 +239,27 @@ def test_gpu_plane_furnace_full_hd_equals_estimator_integral(gpu_renderer, rough
     ro, _ = frames_for(fp, 1, 8)
     img, _ = gpu_render(gpu_renderer, floor_scene(roughness), furnace_env(), W, H, fp, ro)
     check_plane(img, fp, W, H, roughness, rel_tol=0.002)
+
+
+def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
+    """Sky mode (enableEnvMap off): the light sample still comes from the HDR map (RT:1379-1405 has
+    no enableEnvMap test), the escaping BSDF sample sees getDefaultSkyColor unweighted."""
+    W, H, rough = 48, 27, 0.5
+    fp_env = cf.frame_params(W, H, env_intensity=INTENSITY)
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_env_map=False)
+    _, fr_env = frames_for(fp_env, 1, 1)
+    _, frames = frames_for(fp, 1, 64)
+    sd = floor_scene(rough)
+    env_img, _ = oracle_render(sd, furnace_env(), W, H, fr_env)
+    img, _ = oracle_render(sd, furnace_env(), W, H, frames)
+    mu = view_cosines(fp, W, H)
+    on = (np.abs(np.asarray(env_img, np.float64).mean(-1) / float(EXPECT) - 1.0) > 1e-6) & (mu > 0.02)
+    assert on.sum() > 0.2 * W * H
+    grid = np.linspace(0.02, 1.0, 80)
+    terms = [estimator_terms(m, rough) for m in grid]
+    for c in range(3):
+        tab = [float(EXPECT) * A + S[c] for A, _, S in terms]
+        e = np.interp(mu[on], grid, tab)
+        got = np.asarray(img, np.float64)[..., c][on]
+        se = got.std() / np.sqrt(on.sum())
+        assert abs(got.mean() - e.mean()) <= 0.002 * e.mean() + 4 * se, (c, got.mean(), e.mean(), se)
