@@ -34,13 +34,17 @@ G1(V) D / (4 V.z), RT:962; hdrPdf of a constant map 1 / (2 pi^2 sin theta), RT:1
 power-heuristic MIS of RT:1285-1288 on both estimators; the double weight above).  No sampling
 routine enters the integral, so SampleGGXVNDF, SampleHdr, the Sobol/Cranley-Patterson numbers
 and the wavefront bookkeeping are all checked against it: the mean over the floor's pixels must
-equal the integral within the sampling error.
+equal the integral within 0.3% plus the sampling error (measured on the oracle at 480x270x16
+with a 512- or 2048-wide map: 0.05% / 0.14% below it at roughness 0.5 / 0.8, 1-2 standard
+errors; a missing double weight or a pdf off by any factor moves it by 10% and more).
 
 Not covered, by the reference's own design: a dielectric (RT:1429 skips f/pdf on refraction,
 R9) and the Disney diffuse lobe (retro-reflection, albedo != 1) are not energy conserving, and
 with MIS off the light sample and the BSDF sample both count the environment (RT:1396, :1431),
 so those cases have no furnace value to test against.
 """
+from functools import lru_cache
+
 import numpy as np
 import pytest
 
@@ -216,6 +220,15 @@ def check_plane(img, fp, W, H, roughness, rel_tol):
     return got / want
 
 
+@lru_cache(maxsize=1)
+def plane_env():
+    """A constant 1024x512 map: SampleHdr returns texel-centre directions, so the light sample is
+    a quadrature over the map's texels; at 64x32 that quadrature is 0.2-0.4% off the integral,
+    at 512 and above it has converged (0.05% / 0.14% below it at roughness 0.5 / 0.8)."""
+    img = np.full((512, 1024, 3), LE, np.float32)
+    return img, sl.hdr_cache(img)
+
+
 def floor_scene(roughness: float):
     mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=1.0, roughness=roughness, specular=1.0)
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
@@ -226,8 +239,8 @@ def test_oracle_plane_furnace_equals_estimator_integral(roughness):
     W, H = 48, 27
     fp = cf.frame_params(W, H, env_intensity=INTENSITY)
     _, frames = frames_for(fp, 1, 64)
-    img, _ = oracle_render(floor_scene(roughness), furnace_env(), W, H, frames)
-    check_plane(img, fp, W, H, roughness, rel_tol=0.002)
+    img, _ = oracle_render(floor_scene(roughness), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003)
 
 
 @pytest.mark.gpu
@@ -237,8 +250,8 @@ def test_gpu_plane_furnace_full_hd_equals_estimator_integral(gpu_renderer, rough
     W, H = 1920, 1080
     fp = cf.frame_params(W, H, env_intensity=INTENSITY)
     ro, _ = frames_for(fp, 1, 8)
-    img, _ = gpu_render(gpu_renderer, floor_scene(roughness), furnace_env(), W, H, fp, ro)
-    check_plane(img, fp, W, H, roughness, rel_tol=0.002)
+    img, _ = gpu_render(gpu_renderer, floor_scene(roughness), plane_env(), W, H, fp, ro)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003)
 
 
 def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
@@ -250,8 +263,8 @@ def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
     _, fr_env = frames_for(fp_env, 1, 1)
     _, frames = frames_for(fp, 1, 64)
     sd = floor_scene(rough)
-    env_img, _ = oracle_render(sd, furnace_env(), W, H, fr_env)
-    img, _ = oracle_render(sd, furnace_env(), W, H, frames)
+    env_img, _ = oracle_render(sd, plane_env(), W, H, fr_env)
+    img, _ = oracle_render(sd, plane_env(), W, H, frames)
     mu = view_cosines(fp, W, H)
     on = (np.abs(np.asarray(env_img, np.float64).mean(-1) / float(EXPECT) - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H
@@ -262,4 +275,4 @@ def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
         e = np.interp(mu[on], grid, tab)
         got = np.asarray(img, np.float64)[..., c][on]
         se = got.std() / np.sqrt(on.sum())
-        assert abs(got.mean() - e.mean()) <= 0.002 * e.mean() + 4 * se, (c, got.mean(), e.mean(), se)
+        assert abs(got.mean() - e.mean()) <= 0.003 * e.mean() + 4 * se, (c, got.mean(), e.mean(), se)
