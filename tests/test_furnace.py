@@ -155,13 +155,17 @@ def test_gpu_white_furnace_full_hd(gpu_renderer, roughness):
 FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scene.h:116-120): y = const
 
 
-def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800):
+def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800, brdf: bool = False):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
     cancels); B = the escaping BSDF sample with its MIS weight, p_b w_b (f cos / p_b)^2 (RT:1431,
     RT:1496); S[c] = the same sample in sky mode, p_b (f cos / p_b)^2 getDefaultSkyColor(L.y)[c]
-    (RT:1500-1503: no MIS weight, no envIntensity; RT:1190-1193)."""
+    (RT:1500-1503: no MIS weight, no envIntensity; RT:1190-1193).
+    brdf: the BRDF integrator instead (RT:1290-1367, the same three terms at RT:1321, :1338 + :1352,
+    :1356) with BRDF_Evaluate's metal specular (RT:836-920): GTR2(NdotH, roughness^2), Smith G1
+    with alphaG = roughness (RT:876-877, not roughness^2) and the GTR2 half-vector pdf
+    D NdotH / (4 LdotH) of SampleGTR2 (RT:732-749, :911)."""
     a = max(1e-3, roughness * roughness)                       # m.ax = m.ay (RT:205-207)
     th = (np.arange(nth) + 0.5) * (np.pi / 2) / nth
     ph = (np.arange(nph) + 0.5) * (2 * np.pi) / nph
@@ -176,22 +180,31 @@ def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800)
     def G1(w):
         return 2 * w[..., 2] / (w[..., 2] + np.sqrt(a * a * (w[..., 0] ** 2 + w[..., 1] ** 2) + w[..., 2] ** 2))
 
+    if brdf:
+        def G1(w):  # SmithG_GGX(NdotV, alphaG = roughness): a = roughness^2 under the root
+            r2 = roughness * roughness
+            return 2 * w[..., 2] / (w[..., 2] + np.sqrt(r2 + w[..., 2] ** 2 - r2 * w[..., 2] ** 2))
+
     g1v, g1l = G1(V), G1(L)
     fcos = D * g1v * g1l / (4 * mu)       # F D G2 / (4 L.z V.z) * L.z, F = 1
-    pb = g1v * D / (4 * mu)               # VNDF pdf of the reflected direction
+    if brdf:
+        pb = D * Hh[..., 2] / (4 * np.sum(L * Hh, axis=-1))   # GTR2 half-vector pdf
+    else:
+        pb = g1v * D / (4 * mu)           # VNDF pdf of the reflected direction
     pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
     wl = pl ** 2 / (pl ** 2 + pb ** 2)
     t = 0.5 * (np.cos(T) + 1.0)
     sky = [(1 - t) + t * c for c in (0.5, 0.7, 1.0)]
     A = float(np.sum(wl * fcos * dw))
-    B = float(np.sum((1 - wl) * pb * g1l ** 2 * dw))
-    S = np.array([np.sum(pb * g1l ** 2 * sc * dw) for sc in sky])
+    w2 = fcos * fcos / pb                 # p_b (f cos / p_b)^2: the sample's weight applied twice
+    B = float(np.sum((1 - wl) * w2 * dw))
+    S = np.array([np.sum(w2 * sc * dw) for sc in sky])
     return A, B, S
 
 
-def estimator_expectation(mu: float, roughness: float) -> float:
+def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
     """Environment mode, relative to Le * envIntensity: A + B."""
-    A, B, _ = estimator_terms(mu, roughness)
+    A, B, _ = estimator_terms(mu, roughness, brdf=brdf)
     return A + B
 
 
@@ -207,13 +220,13 @@ def view_cosines(fp, W, H):
     return -d[..., 1]
 
 
-def check_plane(img, fp, W, H, roughness, rel_tol):
+def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False):
     v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
     grid = np.linspace(0.02, 1.0, 80)
-    e = np.interp(mu[on], grid, [estimator_expectation(m, roughness) for m in grid])
+    e = np.interp(mu[on], grid, [estimator_expectation(m, roughness, brdf) for m in grid])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -234,24 +247,26 @@ def floor_scene(roughness: float):
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
 
 
+@pytest.mark.parametrize("mode", ["bsdf", "brdf"])
 @pytest.mark.parametrize("roughness", [0.5, 0.8])
-def test_oracle_plane_furnace_equals_estimator_integral(roughness):
+def test_oracle_plane_furnace_equals_estimator_integral(roughness, mode):
     W, H = 48, 27
-    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=(mode == "bsdf"))
     _, frames = frames_for(fp, 1, 64)
     img, _ = oracle_render(floor_scene(roughness), plane_env(), W, H, frames)
-    check_plane(img, fp, W, H, roughness, rel_tol=0.003)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003, brdf=(mode == "brdf"))
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["bsdf", "brdf"])
 @pytest.mark.parametrize("roughness", [0.5, 0.8])
-def test_gpu_plane_furnace_full_hd_equals_estimator_integral(gpu_renderer, roughness):
+def test_gpu_plane_furnace_full_hd_equals_estimator_integral(gpu_renderer, roughness, mode):
     """1920x1080, 8 frames on the GPU against the integral (no oracle): sampling error ~1e-4."""
     W, H = 1920, 1080
-    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=(mode == "bsdf"))
     ro, _ = frames_for(fp, 1, 8)
     img, _ = gpu_render(gpu_renderer, floor_scene(roughness), plane_env(), W, H, fp, ro)
-    check_plane(img, fp, W, H, roughness, rel_tol=0.003)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003, brdf=(mode == "brdf"))
 
 
 def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
