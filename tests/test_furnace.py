@@ -155,7 +155,7 @@ def test_gpu_white_furnace_full_hd(gpu_renderer, roughness):
 FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scene.h:116-120): y = const
 
 
-def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800, brdf: bool = False):
+def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
@@ -202,6 +202,15 @@ def estimator_terms(mu: float, roughness: float, nth: int = 400, nph: int = 800,
     return A, B, S
 
 
+MU_GRID = np.linspace(0.02, 1.0, 80)
+
+
+@lru_cache(maxsize=None)
+def terms_table(roughness: float, brdf: bool = False):
+    """estimator_terms over MU_GRID (the tests interpolate per pixel between these)."""
+    return [estimator_terms(float(m), roughness, brdf=brdf) for m in MU_GRID]
+
+
 def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
     """Environment mode, relative to Le * envIntensity: A + B."""
     A, B, _ = estimator_terms(mu, roughness, brdf=brdf)
@@ -225,8 +234,7 @@ def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False):
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
-    grid = np.linspace(0.02, 1.0, 80)
-    e = np.interp(mu[on], grid, [estimator_expectation(m, roughness, brdf) for m in grid])
+    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf)])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -283,11 +291,9 @@ def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
     mu = view_cosines(fp, W, H)
     on = (np.abs(np.asarray(env_img, np.float64).mean(-1) / float(EXPECT) - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H
-    grid = np.linspace(0.02, 1.0, 80)
-    terms = [estimator_terms(m, rough) for m in grid]
     for c in range(3):
-        tab = [float(EXPECT) * A + S[c] for A, _, S in terms]
-        e = np.interp(mu[on], grid, tab)
+        tab = [float(EXPECT) * A + S[c] for A, _, S in terms_table(rough)]
+        e = np.interp(mu[on], MU_GRID, tab)
         got = np.asarray(img, np.float64)[..., c][on]
         se = got.std() / np.sqrt(on.sum())
         assert abs(got.mean() - e.mean()) <= 0.003 * e.mean() + 4 * se, (c, got.mean(), e.mean(), se)
