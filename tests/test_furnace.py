@@ -20,6 +20,8 @@ every angle, RT:397-405) reflects all the light that its microfacet model keeps,
   0.6: 0.75, 0.8: 0.50 of the furnace); both implementations keep it (R-faithful).
 - the BRDF integrator (enableBSDF off) samples GTR2 half-vectors (RT:1290-1367) and has the
   same double weight (RT:1338 then RT:1352): 1 within 2% at roughness 0.05, monotone after.
+  On the plane its non-metal materials are pinned as well: the Disney diffuse lobe (Fd90
+  retro-reflection) plus the Schlick specular, sampled as a lobe mixture (RT:789-833).
 
 The furnace is a constant 64x32 HDR map (its hdrCache from the same host code as the real
 map's, `rts_hdr_cache`); the object is the reference's bunny mesh in front of the camera.
@@ -155,7 +157,8 @@ def test_gpu_white_furnace_full_hd(gpu_renderer, roughness):
 FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scene.h:116-120): y = const
 
 
-def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False):
+def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False,
+                    metallic: float = 1.0, specular: float = 1.0):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
@@ -188,7 +191,21 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
     g1v, g1l = G1(V), G1(L)
     fcos = D * g1v * g1l / (4 * mu)       # F D G2 / (4 L.z V.z) * L.z, F = 1
     if brdf:
-        pb = D * Hh[..., 2] / (4 * np.sum(L * Hh, axis=-1))   # GTR2 half-vector pdf
+        LdotH = np.sum(L * Hh, axis=-1)
+        pb = D * Hh[..., 2] / (4 * LdotH)   # GTR2 half-vector pdf
+        if metallic < 1.0:
+            # BRDF_Evaluate with base colour 1 (Ctint = 1): Disney diffuse Fd / pi, specular with
+            # Fs = mix(Cspec0, 1, FH), Cspec0 = mix(0.08 * specular, 1, metallic); lobe choice
+            # p_diffuse : p_specular = (1 - metallic) : 1 (CalculateBRDFLobePdfs, RT:520-533)
+            def schlick(u):
+                return np.clip(1.0 - u, 0.0, 1.0) ** 5
+            fd90 = 0.5 + 2.0 * LdotH * LdotH * roughness
+            Fd = (1 + (fd90 - 1) * schlick(L[..., 2])) * (1 + (fd90 - 1) * schlick(mu))
+            cspec0 = 0.08 * specular * (1 - metallic) + metallic
+            Fs = cspec0 + (1 - cspec0) * schlick(LdotH)
+            fcos = ((1 - metallic) * Fd / np.pi) * L[..., 2] + Fs * fcos
+            pd, ps = (1 - metallic) / (2 - metallic), 1 / (2 - metallic)
+            pb = pd * L[..., 2] / np.pi + ps * pb
     else:
         pb = g1v * D / (4 * mu)           # VNDF pdf of the reflected direction
     pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
@@ -206,9 +223,9 @@ MU_GRID = np.linspace(0.02, 1.0, 80)
 
 
 @lru_cache(maxsize=None)
-def terms_table(roughness: float, brdf: bool = False):
+def terms_table(roughness: float, brdf: bool = False, metallic: float = 1.0, specular: float = 1.0):
     """estimator_terms over MU_GRID (the tests interpolate per pixel between these)."""
-    return [estimator_terms(float(m), roughness, brdf=brdf) for m in MU_GRID]
+    return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular) for m in MU_GRID]
 
 
 def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
@@ -229,12 +246,12 @@ def view_cosines(fp, W, H):
     return -d[..., 1]
 
 
-def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False):
+def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0):
     v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
-    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf)])
+    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular)])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -250,8 +267,8 @@ def plane_env():
     return img, sl.hdr_cache(img)
 
 
-def floor_scene(roughness: float):
-    mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=1.0, roughness=roughness, specular=1.0)
+def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0):
+    mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=metallic, roughness=roughness, specular=specular)
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
 
 
@@ -297,3 +314,30 @@ def test_oracle_plane_furnace_sky_mode_equals_estimator_integral():
         got = np.asarray(img, np.float64)[..., c][on]
         se = got.std() / np.sqrt(on.sum())
         assert abs(got.mean() - e.mean()) <= 0.003 * e.mean() + 4 * se, (c, got.mean(), e.mean(), se)
+
+
+# BRDF integrator, non-metals: Disney diffuse (Fd90 retro-reflection) + Schlick specular, lobes
+# picked 1 : 1 (metallic 0) or 1 : 2 (metallic 0.5); (metallic, specular)
+BRDF_MATS = {"plastic": (0.0, 0.5), "diffuse_only_f0": (0.0, 0.0), "half_metal": (0.5, 0.5)}
+
+
+@pytest.mark.parametrize("mat", list(BRDF_MATS))
+@pytest.mark.parametrize("roughness", [0.5, 0.8])
+def test_oracle_plane_furnace_brdf_diffuse_equals_estimator_integral(roughness, mat):
+    met, spec = BRDF_MATS[mat]
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=False)
+    _, frames = frames_for(fp, 1, 64)
+    img, _ = oracle_render(floor_scene(roughness, met, spec), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003, brdf=True, metallic=met, specular=spec)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mat", ["plastic", "half_metal"])
+def test_gpu_plane_furnace_brdf_diffuse_full_hd(gpu_renderer, mat):
+    met, spec = BRDF_MATS[mat]
+    W, H = 1920, 1080
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=False)
+    ro, _ = frames_for(fp, 1, 8)
+    img, _ = gpu_render(gpu_renderer, floor_scene(0.5, met, spec), plane_env(), W, H, fp, ro)
+    check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=met, specular=spec)
