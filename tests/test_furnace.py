@@ -22,6 +22,8 @@ every angle, RT:397-405) reflects all the light that its microfacet model keeps,
   same double weight (RT:1338 then RT:1352): 1 within 2% at roughness 0.05, monotone after.
   On the plane its non-metal materials are pinned as well: the Disney diffuse lobe (Fd90
   retro-reflection) plus the Schlick specular, sampled as a lobe mixture (RT:789-833).
+- the BSDF integrator's non-metals (transmission 0) on the plane: EvalDiffuse + the
+  dielectric-Fresnel EvalSpecReflection with DisneyEval's Fresnel-based lobe weights.
 
 The furnace is a constant 64x32 HDR map (its hdrCache from the same host code as the real
 map's, `rts_hdr_cache`); the object is the reference's bunny mesh in front of the camera.
@@ -158,7 +160,7 @@ FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scen
 
 
 def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False,
-                    metallic: float = 1.0, specular: float = 1.0):
+                    metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
@@ -208,6 +210,30 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
             pb = pd * L[..., 2] / np.pi + ps * pb
     else:
         pb = g1v * D / (4 * mu)           # VNDF pdf of the reflected direction
+        if metallic < 1.0:
+            # DisneyEval of a non-metal, transmission 0, base colour 1 (RT:1010-1067): EvalDiffuse
+            # (Fd90) + EvalSpecReflection with F = mix(specCol, 1, DielectricFresnel(V.H, eta)),
+            # specCol = F0^2 (GetSpecColor, RT:420-427), lobe weights from that same Fresnel
+            # (CalculateBSDFLobePdfs, RT:537-550).  The sample's own pdf (approxFresnel weights)
+            # cancels: history carries f_lobe / p_lobe, the escape multiplies by f / p_eval.
+            eta = 1.0 / ior
+            LdotH = np.sum(L * Hh, axis=-1)
+            VdotH = np.abs(np.sum(V * Hh, axis=-1))
+            sin2 = eta * eta * (1 - VdotH * VdotH)
+            cost = np.sqrt(np.maximum(1 - sin2, 0.0))
+            rs = (eta * cost - VdotH) / (eta * cost + VdotH)
+            rp = (eta * VdotH - cost) / (eta * VdotH + cost)
+            fres = 0.5 * (rs * rs + rp * rp)
+            F0 = ((1 - eta) / (1 + eta)) ** 2
+            Fspec = F0 + (1 - F0) * fres
+
+            def schlick(u):
+                return np.clip(1.0 - u, 0.0, 1.0) ** 5
+            fd90 = 0.5 + 2.0 * LdotH * LdotH * roughness
+            Fd = (1 + (fd90 - 1) * schlick(L[..., 2])) * (1 + (fd90 - 1) * schlick(mu))
+            wd = 1.0 / (1.0 + Fspec)
+            fcos = Fd / np.pi * L[..., 2] + Fspec * fcos
+            pb = wd * L[..., 2] / np.pi + (1 - wd) * pb
     pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
     wl = pl ** 2 / (pl ** 2 + pb ** 2)
     t = 0.5 * (np.cos(T) + 1.0)
@@ -223,9 +249,11 @@ MU_GRID = np.linspace(0.02, 1.0, 80)
 
 
 @lru_cache(maxsize=None)
-def terms_table(roughness: float, brdf: bool = False, metallic: float = 1.0, specular: float = 1.0):
+def terms_table(roughness: float, brdf: bool = False, metallic: float = 1.0, specular: float = 1.0,
+                ior: float = 1.5):
     """estimator_terms over MU_GRID (the tests interpolate per pixel between these)."""
-    return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular) for m in MU_GRID]
+    return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular, ior=ior)
+            for m in MU_GRID]
 
 
 def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
@@ -246,12 +274,12 @@ def view_cosines(fp, W, H):
     return -d[..., 1]
 
 
-def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0):
+def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0, ior=1.5):
     v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
-    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular)])
+    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular, ior)])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -267,8 +295,9 @@ def plane_env():
     return img, sl.hdr_cache(img)
 
 
-def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0):
-    mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=metallic, roughness=roughness, specular=specular)
+def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5):
+    mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=metallic, roughness=roughness, specular=specular,
+                      ior=ior)
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
 
 
@@ -341,3 +370,24 @@ def test_gpu_plane_furnace_brdf_diffuse_full_hd(gpu_renderer, mat):
     ro, _ = frames_for(fp, 1, 8)
     img, _ = gpu_render(gpu_renderer, floor_scene(0.5, met, spec), plane_env(), W, H, fp, ro)
     check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=met, specular=spec)
+
+
+@pytest.mark.parametrize("ior", [1.5, 1.2])
+@pytest.mark.parametrize("roughness", [0.3, 0.8])
+def test_oracle_plane_furnace_bsdf_dielectric_equals_estimator_integral(roughness, ior):
+    """BSDF integrator, non-metal (transmission 0): Disney diffuse + dielectric-Fresnel specular,
+    the eval's lobe weights from that Fresnel, the sample's approxFresnel weights cancelling."""
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    _, frames = frames_for(fp, 1, 64)
+    img, _ = oracle_render(floor_scene(roughness, 0.0, 0.5, ior), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, roughness, rel_tol=0.003, metallic=0.0, ior=ior)
+
+
+@pytest.mark.gpu
+def test_gpu_plane_furnace_bsdf_dielectric_full_hd(gpu_renderer):
+    W, H = 1920, 1080
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    ro, _ = frames_for(fp, 1, 8)
+    img, _ = gpu_render(gpu_renderer, floor_scene(0.5, 0.0, 0.5, 1.5), plane_env(), W, H, fp, ro)
+    check_plane(img, fp, W, H, 0.5, rel_tol=0.003, metallic=0.0, ior=1.5)
