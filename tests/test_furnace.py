@@ -160,7 +160,8 @@ FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scen
 
 
 def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False,
-                    metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5):
+                    metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5,
+                    clearcoat: float = 0.0, gloss: float = 0.5):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
@@ -190,8 +191,12 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
             r2 = roughness * roughness
             return 2 * w[..., 2] / (w[..., 2] + np.sqrt(r2 + w[..., 2] ** 2 - r2 * w[..., 2] ** 2))
 
+    def G1b025(w):  # SmithG_GGX(NdotV, 0.25) of the clearcoat (RT:892)
+        return 2 * w[..., 2] / (w[..., 2] + np.sqrt(0.0625 + w[..., 2] ** 2 - 0.0625 * w[..., 2] ** 2))
+
     g1v, g1l = G1(V), G1(L)
     fcos = D * g1v * g1l / (4 * mu)       # F D G2 / (4 L.z V.z) * L.z, F = 1
+    p_true = None                         # the sampling density, when it is not the eval's pdf
     if brdf:
         LdotH = np.sum(L * Hh, axis=-1)
         pb = D * Hh[..., 2] / (4 * LdotH)   # GTR2 half-vector pdf
@@ -206,8 +211,27 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
             cspec0 = 0.08 * specular * (1 - metallic) + metallic
             Fs = cspec0 + (1 - cspec0) * schlick(LdotH)
             fcos = ((1 - metallic) * Fd / np.pi) * L[..., 2] + Fs * fcos
-            pd, ps = (1 - metallic) / (2 - metallic), 1 / (2 - metallic)
+            rc = (1 - metallic) * 0.25 * clearcoat
+            rsum = (1 - metallic) + 1 + rc
+            pd, ps, pc = (1 - metallic) / rsum, 1 / rsum, rc / rsum
+            ps_spec = pb
             pb = pd * L[..., 2] / np.pi + ps * pb
+            if clearcoat > 0:
+                # clearcoat (RT:890-900): GTR1 with alpha mix(0.1, 0.001, 1 - gloss) in the eval
+                # but mix(0.1, 0.001, gloss) in SampleGTR1 (RT:797, :825): the eval's pdf is not
+                # the sampling density unless gloss = 0.5, and the BRDF integrator divides by the
+                # eval's pdf (RT:1338), so the density enters the expectation (returned as ps_true)
+                def gtr1(c, al):
+                    a2 = al * al
+                    return (a2 - 1) / (np.pi * np.log(a2) * (1 + (a2 - 1) * c * c))
+                ae, as_ = 0.1 + (0.001 - 0.1) * (1 - gloss), 0.1 + (0.001 - 0.1) * gloss
+                Dr = gtr1(Hh[..., 2], ae)
+                Fr = 0.04 + 0.96 * schlick(LdotH)
+                Gr = G1b025(L) * G1b025(V)
+                fcos = fcos + 0.25 * Gr * Fr * Dr * clearcoat / (4 * mu)
+                pb = pb + pc * Dr * Hh[..., 2] / (4 * LdotH)
+                p_true = (pd * L[..., 2] / np.pi + ps * ps_spec
+                          + pc * gtr1(Hh[..., 2], as_) * Hh[..., 2] / (4 * LdotH))
     else:
         pb = g1v * D / (4 * mu)           # VNDF pdf of the reflected direction
         if metallic < 1.0:
@@ -239,7 +263,8 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
     t = 0.5 * (np.cos(T) + 1.0)
     sky = [(1 - t) + t * c for c in (0.5, 0.7, 1.0)]
     A = float(np.sum(wl * fcos * dw))
-    w2 = fcos * fcos / pb                 # p_b (f cos / p_b)^2: the sample's weight applied twice
+    # p_s (f cos / p_b)^2: the sample's weight applied twice (p_s = p_b unless p_true says otherwise)
+    w2 = fcos * fcos / pb if p_true is None else p_true * (fcos / pb) ** 2
     B = float(np.sum((1 - wl) * w2 * dw))
     S = np.array([np.sum(w2 * sc * dw) for sc in sky])
     return A, B, S
@@ -250,10 +275,10 @@ MU_GRID = np.linspace(0.02, 1.0, 80)
 
 @lru_cache(maxsize=None)
 def terms_table(roughness: float, brdf: bool = False, metallic: float = 1.0, specular: float = 1.0,
-                ior: float = 1.5):
+                ior: float = 1.5, clearcoat: float = 0.0, gloss: float = 0.5):
     """estimator_terms over MU_GRID (the tests interpolate per pixel between these)."""
-    return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular, ior=ior)
-            for m in MU_GRID]
+    return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular, ior=ior,
+                            clearcoat=clearcoat, gloss=gloss) for m in MU_GRID]
 
 
 def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
@@ -274,12 +299,13 @@ def view_cosines(fp, W, H):
     return -d[..., 1]
 
 
-def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0, ior=1.5):
+def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0, ior=1.5,
+                clearcoat=0.0, gloss=0.5):
     v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
-    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular, ior)])
+    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular, ior, clearcoat, gloss)])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -295,9 +321,10 @@ def plane_env():
     return img, sl.hdr_cache(img)
 
 
-def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5):
+def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5,
+                clearcoat: float = 0.0, gloss: float = 0.0):
     mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=metallic, roughness=roughness, specular=specular,
-                      ior=ior)
+                      ior=ior, clearcoat=clearcoat, clearcoat_gloss=gloss)
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
 
 
@@ -391,3 +418,15 @@ def test_gpu_plane_furnace_bsdf_dielectric_full_hd(gpu_renderer):
     ro, _ = frames_for(fp, 1, 8)
     img, _ = gpu_render(gpu_renderer, floor_scene(0.5, 0.0, 0.5, 1.5), plane_env(), W, H, fp, ro)
     check_plane(img, fp, W, H, 0.5, rel_tol=0.003, metallic=0.0, ior=1.5)
+
+
+@pytest.mark.parametrize("gloss", [0.1, 0.5, 0.9])
+def test_oracle_plane_furnace_brdf_clearcoat_equals_estimator_integral(gloss):
+    """BRDF integrator with clearcoat 1 (RT:890-900): GTR1 evaluated with alpha
+    mix(0.1, 0.001, 1 - gloss) but sampled with mix(0.1, 0.001, gloss) (RT:797, :825); the
+    integral uses the sampling density where the estimator divides by the eval's pdf."""
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=False)
+    _, frames = frames_for(fp, 1, 64)
+    img, _ = oracle_render(floor_scene(0.5, 0.0, 0.5, 1.5, 1.0, gloss), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=0.0, specular=0.5, clearcoat=1.0, gloss=gloss)
