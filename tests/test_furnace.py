@@ -161,7 +161,7 @@ FLOOR_AT = ((0, 0, 0), (2.2, -2, 3), (14, 7, 7))   # the reference's floor (Scen
 
 def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400, brdf: bool = False,
                     metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5,
-                    clearcoat: float = 0.0, gloss: float = 0.5):
+                    clearcoat: float = 0.0, gloss: float = 0.5, sheen: float = 0.0):
     """The reference BSDF integrator's expectation for one bounce off an F = 1 metal plane
     (normal = +y = the env map's pole axis) viewed at cosine mu, as three hemisphere integrals
     (midpoint rule): A = the light sample, w_l f cos (RT:1380-1405, the constant-map hdrPdf
@@ -210,7 +210,8 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
             Fd = (1 + (fd90 - 1) * schlick(L[..., 2])) * (1 + (fd90 - 1) * schlick(mu))
             cspec0 = 0.08 * specular * (1 - metallic) + metallic
             Fs = cspec0 + (1 - cspec0) * schlick(LdotH)
-            fcos = ((1 - metallic) * Fd / np.pi) * L[..., 2] + Fs * fcos
+            # sheen (RT:894, :898): FH * sheen * Csheen added to the diffuse term, Csheen = 1 here
+            fcos = ((1 - metallic) * (Fd / np.pi + schlick(LdotH) * sheen)) * L[..., 2] + Fs * fcos
             rc = (1 - metallic) * 0.25 * clearcoat
             rsum = (1 - metallic) + 1 + rc
             pd, ps, pc = (1 - metallic) / rsum, 1 / rsum, rc / rsum
@@ -275,10 +276,10 @@ MU_GRID = np.linspace(0.02, 1.0, 80)
 
 @lru_cache(maxsize=None)
 def terms_table(roughness: float, brdf: bool = False, metallic: float = 1.0, specular: float = 1.0,
-                ior: float = 1.5, clearcoat: float = 0.0, gloss: float = 0.5):
+                ior: float = 1.5, clearcoat: float = 0.0, gloss: float = 0.5, sheen: float = 0.0):
     """estimator_terms over MU_GRID (the tests interpolate per pixel between these)."""
     return [estimator_terms(float(m), roughness, brdf=brdf, metallic=metallic, specular=specular, ior=ior,
-                            clearcoat=clearcoat, gloss=gloss) for m in MU_GRID]
+                            clearcoat=clearcoat, gloss=gloss, sheen=sheen) for m in MU_GRID]
 
 
 def estimator_expectation(mu: float, roughness: float, brdf: bool = False) -> float:
@@ -300,12 +301,12 @@ def view_cosines(fp, W, H):
 
 
 def check_plane(img, fp, W, H, roughness, rel_tol, brdf=False, metallic=1.0, specular=1.0, ior=1.5,
-                clearcoat=0.0, gloss=0.5):
+                clearcoat=0.0, gloss=0.5, sheen=0.0):
     v = np.asarray(img, np.float64).mean(axis=-1) / float(EXPECT)
     mu = view_cosines(fp, W, H)
     on = (np.abs(v - 1.0) > 1e-6) & (mu > 0.02)
     assert on.sum() > 0.2 * W * H, on.sum()
-    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular, ior, clearcoat, gloss)])
+    e = np.interp(mu[on], MU_GRID, [A + B for A, B, _ in terms_table(roughness, brdf, metallic, specular, ior, clearcoat, gloss, sheen)])
     got, want = v[on].mean(), e.mean()
     se = v[on].std() / np.sqrt(on.sum())
     assert abs(got - want) <= rel_tol * want + 4 * se, f"roughness {roughness}: {got:.5f} vs {want:.5f} +- {se:.5f}"
@@ -322,9 +323,9 @@ def plane_env():
 
 
 def floor_scene(roughness: float, metallic: float = 1.0, specular: float = 1.0, ior: float = 1.5,
-                clearcoat: float = 0.0, gloss: float = 0.0):
+                clearcoat: float = 0.0, gloss: float = 0.0, sheen: float = 0.0):
     mat = sl.Material(base_color=(1.0, 1.0, 1.0), metallic=metallic, roughness=roughness, specular=specular,
-                      ior=ior, clearcoat=clearcoat, clearcoat_gloss=gloss)
+                      ior=ior, clearcoat=clearcoat, clearcoat_gloss=gloss, sheen=sheen)
     return cf.build_scene((cf.Obj("floor", mat, *FLOOR_AT, False),))
 
 
@@ -427,6 +428,17 @@ def test_oracle_plane_furnace_brdf_clearcoat_equals_estimator_integral(gloss):
     integral uses the sampling density where the estimator divides by the eval's pdf."""
     W, H = 48, 27
     fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=False)
-    _, frames = frames_for(fp, 1, 64)
+    _, frames = frames_for(fp, 1, 256)  # a lobe worth 2-5%: a tighter sampling error
     img, _ = oracle_render(floor_scene(0.5, 0.0, 0.5, 1.5, 1.0, gloss), plane_env(), W, H, frames)
     check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=0.0, specular=0.5, clearcoat=1.0, gloss=gloss)
+
+
+@pytest.mark.parametrize("sheen", [0.5, 1.0])
+def test_oracle_plane_furnace_brdf_sheen_equals_estimator_integral(sheen):
+    """BRDF integrator with sheen (RT:894, :898): FH * sheen * Csheen joins the diffuse term
+    without the 1/pi, sampled by the diffuse lobe."""
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY, enable_bsdf=False)
+    _, frames = frames_for(fp, 1, 256)  # a lobe worth 2-5%: a tighter sampling error
+    img, _ = oracle_render(floor_scene(0.5, 0.0, 0.5, sheen=sheen), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=0.0, specular=0.5, sheen=sheen)
