@@ -257,7 +257,8 @@ def estimator_terms(mu: float, roughness: float, nth: int = 200, nph: int = 400,
             fd90 = 0.5 + 2.0 * LdotH * LdotH * roughness
             Fd = (1 + (fd90 - 1) * schlick(L[..., 2])) * (1 + (fd90 - 1) * schlick(mu))
             wd = 1.0 / (1.0 + Fspec)
-            fcos = Fd / np.pi * L[..., 2] + Fspec * fcos
+            # EvalDiffuse's sheen (RT:943-946): FH * sheen * sheenCol, sheenCol = 1 here
+            fcos = (Fd / np.pi + schlick(LdotH) * sheen) * L[..., 2] + Fspec * fcos
             pb = wd * L[..., 2] / np.pi + (1 - wd) * pb
     pl = 1.0 / (2 * np.pi ** 2 * np.maximum(np.sin(T), 1e-10))
     wl = pl ** 2 / (pl ** 2 + pb ** 2)
@@ -442,3 +443,12 @@ def test_oracle_plane_furnace_brdf_sheen_equals_estimator_integral(sheen):
     _, frames = frames_for(fp, 1, 256)  # a lobe worth 2-5%: a tighter sampling error
     img, _ = oracle_render(floor_scene(0.5, 0.0, 0.5, sheen=sheen), plane_env(), W, H, frames)
     check_plane(img, fp, W, H, 0.5, rel_tol=0.003, brdf=True, metallic=0.0, specular=0.5, sheen=sheen)
+
+
+def test_oracle_plane_furnace_bsdf_sheen_equals_estimator_integral():
+    """BSDF integrator, EvalDiffuse's sheen term (RT:943-946), sampled by the diffuse lobe."""
+    W, H = 48, 27
+    fp = cf.frame_params(W, H, env_intensity=INTENSITY)
+    _, frames = frames_for(fp, 1, 256)
+    img, _ = oracle_render(floor_scene(0.5, 0.0, 0.5, 1.5, sheen=1.0), plane_env(), W, H, frames)
+    check_plane(img, fp, W, H, 0.5, rel_tol=0.003, metallic=0.0, ior=1.5, sheen=1.0)
