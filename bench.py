@@ -43,17 +43,19 @@ METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 L2_PEAK_GBS = 34500.0     # aggregate L2 bandwidth, measured (MI355X_MICROARCH.md §L2)
 N_SIMD = 256 * 4          # CUs x SIMDs
-VALU_CYC = 2              # cycles per wave64 VALU instruction on a SIMD-32 (157.3 TF fp32 = 1024 x 64 x 2.4 GHz)
+VALU_CYC = 2              # cycles per wave64 VALU instruction (MI355X_MICROARCH.md: 32 lanes/cycle x 2)
+SPEC_CLOCK_GHZ = 2.4      # max engine clock (MI355X_MICROARCH.md chip-level parameters)
 # algorithmic bytes per traversal from the reference's visit counts
 #   64 B per internal pop (16 B node ints + two 24-B child AABBs), 16 B per leaf pop,
 #   36 B per triangle test (positions), 132 B per closer-hit update (normals + material),
 #   12 B per HDR texel fetch, 12 B per cache texel fetch, + 24 B per pixel-frame (accum r/w)
 B_INT, B_LEAF, B_TRI, B_UPD, B_ENV, B_CACHE, B_PIXEL = 64, 16, 36, 132, 12, 12, 24
 # wf_trace's own HBM stream per ray (the ~25 MB scene stays in L2 / Infinity Cache): a
-# secondary ray reads its 4-B queue entry and its 32-B origin/direction and writes its 8-B
-# result; a camera ray is rebuilt from the per-pixel camera table (16 B per pixel, shared by
-# the pixel's frames) and writes its 8-B result
-B_RAY_SECONDARY, B_RAY_CAMERA = 4 + 32 + 8, 8
+# secondary ray reads its 4-B queue entry and its 24-B origin/direction (WFState ra/rb or sa/sb:
+# {o.xyz, d.x} float4 + {d.y, d.z} float2) and writes its 8-B result; a camera ray is rebuilt from
+# the per-pixel camera table (16 B per pixel, shared by the pixel's frames) and writes its 8-B
+# result (tests/test_bench_cpu.py pins these to the WFState layout)
+B_RAY_SECONDARY, B_RAY_CAMERA = 4 + 24 + 8, 8
 # wf_trace's own traversal bytes per visit (served from L2 / MALL): a 128-B 4-wide node, a
 # 48-B triangle record
 B_QNODE, B_TRI_REC = 128, 48
@@ -153,18 +155,49 @@ def launch_ranks(n: int, argv) -> int:
 
 
 # ------------------------------------------------------------------------------ CPU baseline
+def host_cpus() -> dict:
+    """The host's cores as this process sees them: the machine's logical CPUs (nproc), the ones
+    this process may run on (affinity), a cgroup CPU quota if one is set, OMP_NUM_THREADS and the
+    CPU model."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["nproc"]
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    info["omp_num_threads"] = int(omp) if omp.isdigit() else None
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                info["cpu_model"] = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(sd, env, W, H, fp, seconds: float, threads: int):
     """The oracle (CPU restatement of the shader, OpenMP) on whole frames 1..k of the same
-    workload until `seconds` of wall time; returns the JSON object and the §8(d) counters."""
+    workload until `seconds` of wall time; returns the JSON object and the §8(d) counters.
+    Threads: --cpu-threads, else every CPU this process may run on, bounded by the CPU share the
+    host grants it (the cgroup quota, or OMP_NUM_THREADS where the pool sets the share that way:
+    16 per GPU on the MI355X pool); the object records all of them."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as orc  # cpu_baseline leg only: the checker, timed as the reference-algorithm baseline
     from rtamd import configs as cf
 
+    host = host_cpus()
     if threads <= 0:
-        try:
-            threads = min(16, len(os.sched_getaffinity(0)))
-        except AttributeError:
-            threads = min(16, os.cpu_count() or 1)
+        threads = host["affinity"]
+        if host["cgroup_cpu_quota"]:
+            threads = min(threads, max(1, int(host["cgroup_cpu_quota"])))
+        if host["omp_num_threads"]:
+            threads = min(threads, host["omp_num_threads"])
     scene = orc.OracleScene(sd.tri_enc, sd.node_enc, env[0], env[1])
     ro = cf.rand_origins(32)
     acc = None
@@ -178,65 +211,97 @@ def cpu_baseline(sd, env, W, H, fp, seconds: float, threads: int):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    obj = {"value": round(tot["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    value = tot["rays"] / dt / 1e6
+    obj = {"value": round(value, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
            "sample": f"oracle/rt_oracle.cpp (CPU restatement of the GLSL path, no culling) on {k} full "
-                     f"{W}x{H} frame(s) of the same workload, {tot['rays']} rays in {dt:.1f} s; "
-                     "llvmpipe GL baseline unavailable (no GL/EGL context, SURVEY §8(c))",
-           "ms_per_frame": round(dt * 1e3 / k, 1)}
+                     f"{W}x{H} frame(s) of the same workload, {tot['rays']} rays in {dt:.1f} s on {threads} "
+                     "OpenMP threads; llvmpipe GL baseline unavailable (no GL/EGL context, SURVEY §8(c))",
+           "ms_per_frame": round(dt * 1e3 / k, 1),
+           "per_core": round(value / threads, 3),
+           "host": host}
     return obj, tot
 
 
 # ------------------------------------------------------------------------------ roofline
 def load_profile(config: str, W: int, H: int, F: int, slots: int):
     """profiles/pmc_<config>.json (tools/profile_gpu.sh + tools/summarize_profile.py): rocprofv3
-    kernel-trace duration and PMC counters of the bench workload's wf_trace launches; used only
-    when its workload key matches this run."""
+    kernel-trace durations and PMC counters of the bench workload's wf_trace and wf_shade
+    launches; used only when its workload key matches this run."""
     p = ROOT / "profiles" / f"pmc_{config}.json"
     if not p.exists():
         return None
     d = json.loads(p.read_text())
-    if (d.get("kernel") == "wf_trace" and d.get("width") == W and d.get("height") == H
-            and d.get("frames_per_step") == F and d.get("path_slots_per_rank") == slots):
+    if (d.get("width") == W and d.get("height") == H and d.get("frames_per_step") == F
+            and d.get("path_slots_per_rank") == slots and "kernels" in d):
         d["_file"] = str(p.relative_to(ROOT))
         return d
     return None
 
 
+# wf_shade's algorithmic HBM bytes per path step (one path shaded in one bounce pass; rt_wavefront.h
+# shade_path, path-state layout DESIGN.md §3): a continuing path reads its active-list entry (4 B),
+# s5 (8), s0 + s2 (32), its two 8-B results (16) and its 24-B continuation ray = 84 B, and writes
+# s0 + s2 + s5 (40), the next continuation and shadow rays (48), two queue entries and an active
+# entry (12) = 100 B.  The s1/s3 rows (Lo, NEE, up to 64 B more) are left out: PF_ZLO paths skip
+# them.  So 184 B is a lower bound per path step; the count of path steps comes from the device
+# (rt_stats.path_steps: the active paths of every shade pass).
+B_SHADE_STEP = 84 + 100
+B_SHADE_FINAL = 16    # the final colour of each sample (fin), blended later
+
+
 def roofline(st, vis, cnt, prof, trace_ms):
-    """wf_trace (the dominant kernel) against the HBM roofline, with its algorithmic HBM bytes:
-    the path-state stream it must move (per ray, B_RAY_*; the scene is cache-resident).
-    traffic = rocprofv3 PMC HBM bytes per launch.  Also: the same kernel's VALU issue rate (its
-    actual limiter), its own traversal bytes against the L2 bandwidth that serves them, and the
-    reference-equivalent §8(d) figure (reference visit counts), labelled as such, never as frac."""
+    """wf_trace (the dominant kernel) priced against the HBM roofline (this path has no MFMA):
+    achieved = its algorithmic HBM bytes (the path-state stream it must move, B_RAY_*; the scene
+    is cache-resident) per launch / the launch time; traffic = rocprofv3 PMC HBM bytes per launch.
+    `limiter` names what actually bounds the kernel, from the measured utilisations: VALU issue at
+    the 2.4 GHz spec clock (standalone launch time of the PMC passes, kernels serialised), L2
+    bandwidth of its own traversal bytes, HBM.  `kernels.wf_shade`: the memory-bound shade against
+    the same HBM peak.  `reference_equivalent`: SURVEY §8(d)'s bytes of the reference's exhaustive
+    traversal, labelled as such and never used as frac."""
     launches = max(1, st["trace_launches"])
     rays_l = st["rays"] / launches
     cam_l = st["samples"] / launches                      # one camera ray per sample
     alg = (B_RAY_SECONDARY * (rays_l - cam_l) + B_RAY_CAMERA * cam_l)
     sec = trace_ms * 1e-3
-    out = {"bound": "hbm", "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-           "kernel": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "rays_per_launch": round(rays_l),
-           "algorithmic_bytes_per_launch": round(alg),
+    out = {"bound": "hbm", "limiter": None, "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "wf_trace", "avg_launch_ms": round(trace_ms, 4),
+           "avg_launch_ms_note": "HIP events on the launch stream during the timed steps (the other frame "
+                                 "group's wf_shade co-runs)",
+           "rays_per_launch": round(rays_l), "algorithmic_bytes_per_launch": round(alg),
            "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "camera": B_RAY_CAMERA}}
-    if prof:
-        out["traffic"] = prof.get("hbm_bytes_per_launch")
+    util = {"hbm": out["frac"]}
+    pt = (prof or {}).get("kernels", {}).get("wf_trace")
+    if pt:
+        out["traffic"] = pt.get("hbm_bytes_per_launch")
         out["profile"] = prof["_file"]
-        out["profile_avg_launch_ms"] = prof.get("avg_launch_ms")
-        sq = prof.get("SQ", {})
-        pl = prof.get("avg_launch_ms") or trace_ms
-        clk = prof.get("clock_ghz") or 2.4
-        if sq.get("SQ_INSTS_VALU"):
-            v = {"insts_per_launch": round(sq["SQ_INSTS_VALU"]), "cycles_per_inst": VALU_CYC, "clock_ghz": clk,
-                 "issue_frac": round(sq["SQ_INSTS_VALU"] * VALU_CYC / (N_SIMD * clk * 1e9 * pl * 1e-3), 4),
-                 "insts_per_ray": round(sq["SQ_INSTS_VALU"] / rays_l, 1)}
+        out["profile_avg_launch_ms"] = pt.get("avg_launch_ms")
+        sa = pt.get("avg_launch_ms_standalone")
+        out["avg_launch_ms_standalone"] = sa
+        sq = pt.get("SQ", {})
+        if sq.get("SQ_INSTS_VALU") and sa:
+            issue = sq["SQ_INSTS_VALU"] * VALU_CYC / (N_SIMD * SPEC_CLOCK_GHZ * 1e9 * sa * 1e-3)
+            v = {"insts_per_launch": round(sq["SQ_INSTS_VALU"]), "insts_per_ray": round(sq["SQ_INSTS_VALU"] / rays_l, 1),
+                 "cycles_per_inst": VALU_CYC, "issue_frac_at_spec_clock": round(issue, 4),
+                 "spec_clock_ghz": SPEC_CLOCK_GHZ}
+            if pt.get("effective_clock_ghz"):
+                v["effective_clock_ghz"] = pt["effective_clock_ghz"]
+                v["issue_frac_at_effective_clock"] = round(issue * SPEC_CLOCK_GHZ / pt["effective_clock_ghz"], 4)
             if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("SQ_THREAD_CYCLES_VALU"):
                 v["lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64 * sq["SQ_ACTIVE_INST_VALU"]), 4)
+            if pt.get("wave_cycle_split"):
+                v["wave_cycle_split"] = pt["wave_cycle_split"]
             out["valu"] = v
+            util["valu_issue"] = v["issue_frac_at_spec_clock"]
     if vis and vis.get("rays"):
         own = (B_QNODE * vis["internal_pops"] + B_TRI_REC * vis["tri_tests"]) / vis["rays"]
+        t_l2 = (out.get("avg_launch_ms_standalone") or trace_ms) * 1e-3
         out["l2"] = {"own_traversal_bytes_per_ray": round(own, 1),
-                     "achieved": round(own * rays_l / sec / 1e9, 1), "peak": L2_PEAK_GBS,
-                     "frac": round(own * rays_l / sec / 1e9 / L2_PEAK_GBS, 4)}
+                     "achieved": round(own * rays_l / t_l2 / 1e9, 1), "peak": L2_PEAK_GBS,
+                     "frac": round(own * rays_l / t_l2 / 1e9 / L2_PEAK_GBS, 4)}
+        util["l2"] = out["l2"]["frac"]
+    out["limiter"] = max(util, key=util.get)
+    out["utilisation"] = util
     if cnt:
         per_ray = (B_INT * cnt["internal_pops"] + B_LEAF * cnt["leaf_pops"] + B_TRI * cnt["tri_tests"] +
                    B_UPD * cnt["closer_updates"]) / cnt["rays"]
@@ -244,6 +309,23 @@ def roofline(st, vis, cnt, prof, trace_ms):
             "bytes_per_ray": round(per_ray, 1), "gbs": round(per_ray * rays_l / sec / 1e9, 1),
             "note": "SURVEY §8(d) bytes of the reference's own exhaustive traversal (oracle visit counts) per "
                     "ray traced here; the device traversal visits fewer nodes, so this is not a bandwidth"}
+    ps = (prof or {}).get("kernels", {}).get("wf_shade")
+    if ps and ps.get("avg_launch_ms_standalone") and st.get("path_steps"):
+        shade_launches = max(1, st["trace_launches"])  # one wf_shade per wf_trace launch
+        steps_l = st["path_steps"] / shade_launches
+        alg_s = B_SHADE_STEP * steps_l + B_SHADE_FINAL * st["samples"] / shade_launches
+        t_s = ps["avg_launch_ms_standalone"] * 1e-3
+        out["kernels"] = {"wf_shade": {
+            "bound": "hbm", "achieved": round(alg_s / t_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg_s / t_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": ps.get("hbm_bytes_per_launch"),
+            "traffic_frac": (round(ps["hbm_bytes_per_launch"] / t_s / 1e9 / HBM_PEAK_GBS, 4)
+                             if ps.get("hbm_bytes_per_launch") else None),
+            "avg_launch_ms_standalone": ps["avg_launch_ms_standalone"],
+            "avg_launch_ms_corunning": ps.get("avg_launch_ms"),
+            "algorithmic_bytes_per_path_step": B_SHADE_STEP, "path_steps_per_launch": round(steps_l),
+            "note": "algorithmic bytes = a lower bound of the path-state rows a step moves (184 B/path step, "
+                    "s1/s3 rows excluded); time = the PMC passes' standalone launches (kernels serialised)",
+            "profile": prof["_file"]}}
     return out
 
 

@@ -112,6 +112,7 @@ typedef struct rt_stats {
   double trace_ms;          /* summed duration of those launches (HIP events around each) */
   uint64_t trace_iters;     /* RT_FLAG_COUNT_VISITS: traversal loop iterations, all waves */
   uint64_t trace_iters_max; /* RT_FLAG_COUNT_VISITS: max loop iterations of one wave       */
+  uint64_t path_steps;      /* wavefront path: shade steps (one per path per bounce pass)  */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

@@ -45,9 +45,17 @@ struct rt_ctx {
   // env
   float4* d_hdr = nullptr;
   float2* d_cache = nullptr;                  // hdrCache.rg; d_hdr = {hdrMap.rgb, hdrCache.b}
-  float4* d_light = nullptr;                  // NEE light samples per hdrCache texel (rt_light_table_kernel)
-  bool light_valid = false;
-  float light_angle = 0.0f;                   // the envAngle d_light was built for
+  // NEE light samples per hdrCache texel (rt_light_table_kernel) for one envAngle each: two tables,
+  // so a call whose angle differs from the previous call's rebuilds the other table on its own
+  // stream after the last call that read that one (an event), without draining calls in flight
+  struct LightTable {
+    float4* d = nullptr;
+    bool valid = false;
+    float angle = 0.0f;                       // the envAngle d was built for
+    hipEvent_t last_use = nullptr;            // on the ctx stream after the last call that read d
+  };
+  LightTable light[2];
+  int light_cur = 0;                          // the table the last call used
   int hdr_w = 0, hdr_h = 0, hdr_res = 0;
   bool env_set = false;
   // frame
@@ -76,10 +84,7 @@ struct rt_ctx {
     hipEvent_t ev = nullptr;                  // the last upload (the host table is reused after it)
   };
   FrameTable ft[5];
-  int trace_mode = 0;                         // rtd::TraceMode of passes >= 1 (secondary rays)
-  int trace_mode0 = 0;                        // rtd::TraceMode of pass 0 (coherent camera rays)
   int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
-  int stagger = -1;                           // >= 0: group g starts after group g-1's pass `stagger` (measured slower)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
@@ -95,7 +100,6 @@ struct rt_ctx {
   // bounces overlaps the other's busy passes; blends stay in frame order (events).
   static constexpr int MAX_GROUPS = 4;
   int n_groups = 2;
-  int stages = 1;                  // frames of a group start over this many passes (RT_STAGES)
   rtd::WFState wfg[MAX_GROUPS]{};
   hipStream_t aux[MAX_GROUPS] = {};
   unsigned int* d_pix = nullptr;   // pixel list of this rank: xy then accumulation index
@@ -144,6 +148,21 @@ struct rt_ctx {
 };
 
 namespace {
+
+// Development settings (measurement and test builds only).  The release library honours only the
+// C-ABI (include/rt_abi.h); `make` also builds lib/librtamd_dev.so with -DRT_DEV, where these
+// environment variables reach the code they name: the test-only culling switch of
+// tests/test_gpu_cull.py (RT_CULL_EPS_SCALE), the traversal-structure variants the parity tests
+// cover (RT_BVH_WIDTH, RT_REBUILD, RT_COLLAPSE, RT_QBFS) and the occupancy / grouping / finisher
+// parameters the A/B tools sweep.
+inline const char* knob(const char* name) {
+#ifdef RT_DEV
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 int fail(rt_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -377,7 +396,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
   std::vector<GNode> rebuilt;
   int croot = root;
   const std::vector<GNode>* T = &gn;
-  const char* re = getenv("RT_REBUILD");
+  const char* re = knob("RT_REBUILD");
   if (!is_leaf(root) && !(re && atoi(re) == 0)) {
     croot = rebuild_over_leaves(gn, root, rebuilt);
     T = &rebuilt;
@@ -401,7 +420,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
   // fixed): f(n, k) = least area of 4-wide roots covering n's subtree with at most k slots,
   // f(n, 1) = A(n) + min_j f(L, j) + f(R, 4 - j), f(n, k) = min(f(n, 1), min_j f(L, j) + f(R, k - j)).
   // RT_COLLAPSE=greedy: open the largest-area internal slot until there are four.
-  const char* ce = getenv("RT_COLLAPSE");
+  const char* ce = knob("RT_COLLAPSE");
   const bool greedy = ce && strcmp(ce, "greedy") == 0;
   const size_t nb = T->size();
   std::vector<double> f(nb * 5, 0.0);
@@ -493,7 +512,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     return idx;
   };
   qroot = is_leaf(croot) ? croot : build(croot, 1);
-  const char* qb = getenv("RT_QBFS");
+  const char* qb = knob("RT_QBFS");
   if (!is_leaf(qroot) && !(qb && atoi(qb) == 0)) {
     // breadth-first numbering (RT_QBFS=0: depth-first): the top levels of the tree are the
     // first nodes (RT_DEBUG_PASSES reports node visits by this index)
@@ -542,63 +561,28 @@ int occupancy(rt_ctx* c) {
   c->block_lds = lds;
   // wavefront traversal: short LDS stack + global overflow
   int kl = 8;  // 16 KiB per block: LDS leaves room for 8 waves/SIMD (12 entries: 6; C3 5853 -> 5959 at 10, 6155 at 8 with the dual schedule at 8 waves)
-  if (const char* e = getenv("RT_LDS_STACK")) kl = atoi(e);
+  if (const char* e = knob("RT_LDS_STACK")) kl = atoi(e);
   kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
   bpc = 0;
-  // measured per pass on C3: coherent camera rays preferred the speculative while-while schedule
-  // and incoherent secondary rays the dual-front one (tools/exp_dual2.sh); with pixel-major
-  // slots a camera-pass wave traces one ray 64 times and the dual schedule is as good (+0.3%)
-  c->trace_mode0 = rtd::TM_DUAL;
-  c->trace_mode = rtd::TM_DUAL;
-  if (const char* e = getenv("RT_TRACE_MODE")) c->trace_mode0 = c->trace_mode = std::max(0, std::min(3, atoi(e)));
-  if (const char* e = getenv("RT_TRACE_MODE0")) c->trace_mode0 = std::max(0, std::min(3, atoi(e)));
-  // persistent grids: as many blocks as can be resident, per schedule (their register counts differ)
-  auto occ = [&](int mode, bool cam) {
+  // persistent grids: as many blocks as can be resident (the camera pass's instantiation and the
+  // secondary passes' one may differ in registers)
+  auto occ = [&](bool cam) {
     int b = 0;
-    hipError_t e;
-    switch (mode * 2 + (cam ? 1 : 0)) {
-      case rtd::TM_IFIF * 2:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true, false>, 256, c->trace_lds);
-        break;
-      case rtd::TM_IFIF * 2 + 1:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_IFIF, true, true>, 256, c->trace_lds);
-        break;
-      case rtd::TM_WW * 2:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true, false>, 256, c->trace_lds);
-        break;
-      case rtd::TM_WW * 2 + 1:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_WW, true, true>, 256, c->trace_lds);
-        break;
-      case rtd::TM_DUAL * 2:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true, false>, 256, c->trace_lds);
-        break;
-      case rtd::TM_DUAL * 2 + 1:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_DUAL, true, true>, 256, c->trace_lds);
-        break;
-      case rtd::TM_SPEC * 2:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, false>, 256, c->trace_lds);
-        break;
-      default:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, true>, 256, c->trace_lds);
-    }
+    const hipError_t e =
+        cam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, true>, 256, c->trace_lds)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, false>, 256, c->trace_lds);
     return e == hipSuccess ? std::max(1, b) : 1;
   };
-  c->trace_bpc0 = occ(c->trace_mode0, true);  // pass 0 is the implicit camera pass
-  c->trace_bpc = occ(c->trace_mode, false);
+  c->trace_bpc0 = occ(true);  // pass 0 is the implicit camera pass
+  c->trace_bpc = occ(false);
   bpc = c->trace_bpc;
-  if (const char* e = getenv("RT_TRACE_BPC")) c->trace_bpc0 = c->trace_bpc = std::max(1, atoi(e));
-  if (const char* e = getenv("RT_POOL_CHUNK")) c->pool_chunk = std::max(64, atoi(e) / 64 * 64);
-  if (getenv("RT_DEBUG")) {
+  if (const char* e = knob("RT_TRACE_BPC")) c->trace_bpc0 = c->trace_bpc = std::max(1, atoi(e));
+  if (const char* e = knob("RT_POOL_CHUNK")) c->pool_chunk = std::max(64, atoi(e) / 64 * 64);
+  if (knob("RT_DEBUG"))
     fprintf(stderr, "[rt] trace: lds entries %d (%d B/block), occupancy API %d blocks/CU, using %d (pass 0: %d); "
             "megakernel %d\n", kl, c->trace_lds, bpc, c->trace_bpc, c->trace_bpc0, c->blocks_per_cu);
-    for (int l = 0; l <= 40960; l += 8192) {
-      int b = 0;
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, rtd::TM_SPEC, true, true>, 256, l);
-      fprintf(stderr, "[rt]   occupancy(lds=%d) = %d\n", l, b);
-    }
-  }
   {
     int b = 0;
     const hipError_t e = c->wide
@@ -606,11 +590,11 @@ int occupancy(rt_ctx* c) {
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_finish<true, false>, 256, c->trace_lds);
     // the finisher's lanes index the traversal overflow column: never more than the trace grid
     c->finish_bpc = std::max(1, std::min(e == hipSuccess ? b : 1, std::max(c->trace_bpc, c->trace_bpc0)));
-    if (const char* fe = getenv("RT_FINISH_BPC")) c->finish_bpc = std::max(1, std::min(c->finish_bpc, atoi(fe)));
+    if (const char* fe = knob("RT_FINISH_BPC")) c->finish_bpc = std::max(1, std::min(c->finish_bpc, atoi(fe)));
     c->pipe_finish_bpc = 2;
-    if (const char* fe = getenv("RT_PIPE_FINISH_BPC")) c->pipe_finish_bpc = std::max(1, atoi(fe));
+    if (const char* fe = knob("RT_PIPE_FINISH_BPC")) c->pipe_finish_bpc = std::max(1, atoi(fe));
     c->pipe_finish_bpc = std::min(c->pipe_finish_bpc, c->finish_bpc);
-    if (getenv("RT_DEBUG"))
+    if (knob("RT_DEBUG"))
       fprintf(stderr, "[rt] wf_finish: occupancy API %d blocks/CU, using %d (pipelined calls %d)\n", b, c->finish_bpc,
               c->pipe_finish_bpc);
   }
@@ -627,26 +611,17 @@ int occupancy(rt_ctx* c) {
 
 template <bool COUNT, bool WIDE>
 void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
-  const int mode = WP.pass == 0 ? c->trace_mode0 : c->trace_mode;
-  if (small && !COUNT && WIDE && mode == rtd::TM_DUAL) {  // static first shares of mid-size passes
+  if (small && !COUNT && WIDE) {  // static first shares of mid-size passes
     if (WP.cam_n)
-      hipLaunchKernelGGL((rtd::wf_trace<false, rtd::TM_DUAL, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
     else
-      hipLaunchKernelGGL((rtd::wf_trace<false, rtd::TM_DUAL, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
     return;
   }
-#define RT_LAUNCH_TRACE(M)                                                                                  \
-  if (WP.cam_n)                                                                                           \
-    hipLaunchKernelGGL((rtd::wf_trace<COUNT, M, WIDE, true>), grid, dim3(256), c->trace_lds, st, WP);      \
-  else                                                                                                    \
-    hipLaunchKernelGGL((rtd::wf_trace<COUNT, M, WIDE, false>), grid, dim3(256), c->trace_lds, st, WP);
-  switch (mode) {
-    case rtd::TM_IFIF: RT_LAUNCH_TRACE(rtd::TM_IFIF) break;
-    case rtd::TM_WW: RT_LAUNCH_TRACE(rtd::TM_WW) break;
-    case rtd::TM_DUAL: RT_LAUNCH_TRACE(rtd::TM_DUAL) break;
-    default: RT_LAUNCH_TRACE(rtd::TM_SPEC)
-  }
-#undef RT_LAUNCH_TRACE
+  if (WP.cam_n)
+    hipLaunchKernelGGL((rtd::wf_trace<COUNT, WIDE, true>), grid, dim3(256), c->trace_lds, st, WP);
+  else
+    hipLaunchKernelGGL((rtd::wf_trace<COUNT, WIDE, false>), grid, dim3(256), c->trace_lds, st, WP);
 }
 
 template <bool COUNT>
@@ -678,8 +653,10 @@ hipEvent_t take_event(rt_ctx* c) {
 int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap) {
   if (ev.size() <= cap) return RT_OK;
   const size_t n = ev.size() - cap / 2;
-  HIPCHK(c, hipEventSynchronize(ev[n - 1].second));
   for (size_t i = 0; i < n; i++) {
+    // pairs of one call can sit on different streams (frame / pixel groups, pipelined sets), so
+    // each pair is waited for itself (in queue order: cheap once the first is done)
+    HIPCHK(c, hipEventSynchronize(ev[i].second));
     float ms = 0.0f;
     HIPCHK(c, hipEventElapsedTime(&ms, ev[i].first, ev[i].second));
     acc_ms += ms;
@@ -697,7 +674,7 @@ constexpr size_t kMaxPendingEvents = 4096;
 // frames 0.94 ms/frame; 161 vs 80 frames +1.8%, all 512 of a bench step at once +2.2%).
 void update_frames_cap(rt_ctx* c, size_t nv) {
   size_t max_slots = size_t(320) << 20;  // 192 B each: 64 GB of the 288 GB HBM3E
-  if (const char* e = getenv("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
+  if (const char* e = knob("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
   if (c->max_slots_req) max_slots = c->max_slots_req;
   c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / std::max<size_t>(1, nv)));
 }
@@ -759,12 +736,10 @@ int rt_create(int hip_device, rt_ctx** out) {
   c->n_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RT_ERR_HIP; }
   c->own_stream = true;
-  if (const char* e = getenv("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
-  if (const char* e = getenv("RT_STAGES")) c->stages = std::max(1, std::min(64, atoi(e)));
-  if (const char* e = getenv("RT_STAGGER")) c->stagger = std::max(-1, atoi(e));
-  if (const char* e = getenv("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
-  if (const char* e = getenv("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
-  if (const char* e = getenv("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
+  if (const char* e = knob("RT_GROUPS")) c->n_groups = std::max(1, std::min(rt_ctx::MAX_GROUPS, atoi(e)));
+  if (const char* e = knob("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
+  if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
+  if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
@@ -783,7 +758,11 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
-  dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_light); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
+  for (auto& t : c->light) {
+    dfree(t.d);
+    if (t.last_use) (void)hipEventDestroy(t.last_use);
+  }
+  dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
@@ -913,7 +892,7 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
   int qroot = root, qdepth = 1;
   bool wide = false;
   if (has) wide = build_wide(gn, root, trin, qn, qroot, qdepth);
-  if (const char* e = getenv("RT_BVH_WIDTH")) if (atoi(e) == 2) wide = false;
+  if (const char* e = knob("RT_BVH_WIDTH")) if (atoi(e) == 2) wide = false;
   if (gn.empty()) {
     GNode z;
     memset(&z, 0, sizeof(z));
@@ -1026,9 +1005,11 @@ int rt_set_env(rt_ctx* c, const float* hdr, const float* cache, int32_t w, int32
   int rc;
   if ((rc = upload(c, (void**)&c->d_hdr, a.data(), a.size() * sizeof(float4)))) return rc;
   if ((rc = upload(c, (void**)&c->d_cache, b.data(), b.size() * sizeof(float2)))) return rc;
-  dfree(c->d_light);
-  HIPCHK(c, hipMalloc(&c->d_light, a.size() * 2 * sizeof(float4)));
-  c->light_valid = false;
+  for (auto& t : c->light) {  // (drained above: no call reads them)
+    dfree(t.d);
+    HIPCHK(c, hipMalloc(&t.d, a.size() * 2 * sizeof(float4)));
+    t.valid = false;
+  }
   c->hdr_w = w; c->hdr_h = h; c->hdr_res = res;
   c->env_set = true;
   return RT_OK;
@@ -1198,7 +1179,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   }
   // a pipelined call (rt_set_pipeline): see rt_ctx::pipe_depth.  One-frame calls, and calls of
   // one batch (at most frames_cap frames) whose whole path state fits in each set.
-  static const bool pix_ok = !getenv("RT_PIX_SPLIT") || atoi(getenv("RT_PIX_SPLIT")) != 0;
+  static const bool pix_ok = !knob("RT_PIX_SPLIT") || atoi(knob("RT_PIX_SPLIT")) != 0;
   const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
   const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
   bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && n_trace_pre > 0 &&
@@ -1300,20 +1281,29 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
                        n_traced);
     HIPCHK(c, hipGetLastError());
   }
-  // NEE light table for this call's envAngle (SampleHdrLight); built with nothing in flight, since
-  // pipelined calls do not wait for the ctx stream
-  if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL) &&
-      (!c->light_valid || __builtin_memcmp(&c->light_angle, &fp->env_angle, sizeof(float)) != 0)) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (auto& a : c->aux) if (a) HIPCHK(c, hipStreamSynchronize(a));
-    const rtd::Env E{c->d_hdr, c->d_cache, c->d_light, c->hdr_w, c->hdr_h, c->hdr_res, fp->env_angle, fp->env_intensity};
-    const unsigned int n = (unsigned int)(c->hdr_w * c->hdr_h);
-    hipLaunchKernelGGL(rtd::rt_light_table_kernel, dim3(std::max(1u, std::min(4096u, (n + 255) / 256))), dim3(256), 0,
-                       c->stream, E, c->d_light);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->light_angle = fp->env_angle;
-    c->light_valid = true;
+  // NEE light table for this call's envAngle (SampleHdrLight): the table built for this angle, or
+  // the other one rebuilt on this call's stream once the last call that read it has finished (a
+  // device-side wait: an interactive envAngle drag keeps its frames in flight)
+  rt_ctx::LightTable* LT = &c->light[c->light_cur];
+  if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
+    auto same = [&](const rt_ctx::LightTable& t) {
+      return t.valid && __builtin_memcmp(&t.angle, &fp->env_angle, sizeof(float)) == 0;
+    };
+    if (!same(*LT)) {
+      const int other = c->light_cur ^ 1;
+      LT = &c->light[other];
+      c->light_cur = other;
+      if (!same(*LT)) {
+        if (LT->last_use) HIPCHK(c, hipStreamWaitEvent(ps, LT->last_use, 0));
+        const rtd::Env E{c->d_hdr, c->d_cache, LT->d, c->hdr_w, c->hdr_h, c->hdr_res, fp->env_angle, fp->env_intensity};
+        const unsigned int n = (unsigned int)(c->hdr_w * c->hdr_h);
+        hipLaunchKernelGGL(rtd::rt_light_table_kernel, dim3(std::max(1u, std::min(4096u, (n + 255) / 256))), dim3(256),
+                           0, ps, E, LT->d);
+        HIPCHK(c, hipGetLastError());
+        LT->angle = fp->env_angle;
+        LT->valid = true;
+      }
+    }
   }
   int done = 0;
   while (done < n_traced) {
@@ -1346,12 +1336,12 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const double eps = 2.0 * (c->cull_K * 0x1p-24 * R * (1.0 + 0x1p-10) + c->cull_off) * (1.0 + 0x1p-9);
       // RT_CULL_EPS_SCALE (tests only): 0 restores the round-1 heuristic margin, whose hole
       // tests/test_gpu_cull.py demonstrates
-      const char* es = getenv("RT_CULL_EPS_SCALE");
+      const char* es = knob("RT_CULL_EPS_SCALE");
       const double sc = es ? atof(es) : 1.0;
       P.cull_eps = (eps * sc < 1e30) ? (float)(eps * sc) : INFINITY;
     }
     P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
-    P.hdr = c->d_hdr; P.cache = c->d_cache; P.light = c->d_light;
+    P.hdr = c->d_hdr; P.cache = c->d_cache; P.light = LT->d;
     P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
     if (P.n_work == 0) continue;
@@ -1376,16 +1366,21 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       // passes still overlap each other
       const bool pix_split = !pipe && pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
       const int G = pipe ? 1 : pix_split ? c->n_groups : std::min(c->n_groups, nf);
-      static const bool debug_passes = getenv("RT_DEBUG_PASSES") != nullptr;
       const unsigned int trace_grid = (unsigned)(c->n_cus * std::max(c->trace_bpc, c->trace_bpc0));
       const unsigned int trace_grid0 = (unsigned)(c->n_cus * c->trace_bpc0);
       const unsigned int trace_grid1 = (unsigned)(c->n_cus * c->trace_bpc);
-      static unsigned long long* d_wave_log = nullptr;  // debug only (RT_DEBUG_PASSES), never freed
+#ifdef RT_DEV  // RT_DEBUG_PASSES: per-pass report of the COUNT build (syncs after every pass)
+      static const bool debug_passes = knob("RT_DEBUG_PASSES") != nullptr;
+      static unsigned long long* d_wave_log = nullptr;  // never freed
       std::vector<unsigned long long> wave_log;
       if (debug_passes) {
         if (!d_wave_log) HIPCHK(c, hipMalloc(&d_wave_log, (size_t)trace_grid * 4 * 4 * sizeof(unsigned long long)));
         wave_log.resize((size_t)trace_grid * 4 * 4);
       }
+#else
+      constexpr bool debug_passes = false;
+      unsigned long long* d_wave_log = nullptr;
+#endif
       const size_t ovf_group = c->stack_ovf_bytes / sizeof(int2) / (size_t)c->n_groups;
       rtd::WFParams WG[rt_ctx::MAX_GROUPS];
       hipStream_t sg[rt_ctx::MAX_GROUPS];
@@ -1408,7 +1403,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         float4* cam = c->wf.cam + (pipe ? (size_t)pset * (size_t)c->n_valid : 0);
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)set * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
-        WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds, or RT_TRACE_WAVELOG builds
+        WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds (RT_DEBUG_PASSES)
         WP.S = c->wfg[set];
         WP.S.pix_xy = c->wf.pix_xy + w0;
         WP.S.pix_acc = c->wf.pix_acc + w0;
@@ -1436,38 +1431,21 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         for (int g = 1; g < G; g++) HIPCHK(c, hipStreamWaitEvent(sg[g], es, 0));
         c->event_pool.push_back(es);  // reusable once the waits are enqueued
       }
-      // Groups are staggered: group g starts once group g-1 has finished pass `stagger`, so
-      // its busy early passes fill the CUs that group g-1's latency-bound late passes leave idle.
       const int last_pass = std::max(0, fp->max_bounce);
       const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
-      hipEvent_t prev_stagger = nullptr, prev_blend = nullptr;
+      hipEvent_t prev_blend = nullptr;
       for (int g = 0; g < G; g++) {
         rtd::WFParams& WP = WG[g];
-        if (prev_stagger) {  // (pixel groups start together: nothing to wait for)
-          HIPCHK(c, hipStreamWaitEvent(sg[g], prev_stagger, 0));
-          c->event_pool.push_back(prev_stagger);  // reusable once the wait is enqueued
-        }
         HIPCHK(c, hipMemsetAsync(WP.S.cnt, 0, 64, sg[g]));
-        prev_stagger = nullptr;
-        // the group's frames start in `stages` steps, one per pass (see wf_gen)
-        const int nfg = WP.n_frames;
-        const int stages = std::max(1, std::min(c->stages, nfg));
         // small groups (one frame per call) end their paths in wf_finish after pass finish_pass-1
         const int fin_pass = (pipe && c->pipe_finish_pass >= 0) ? c->pipe_finish_pass : c->finish_pass;
-        const bool finish = stages == 1 && !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
+        const bool finish = !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
                             fin_pass >= 1 && fin_pass <= last_pass &&
                             ((fp->flags & RT_FLAG_FINISH) || slots_g[g] <= c->finish_slots);
-        for (int pass = 0; pass <= last_pass + stages - 1; pass++) {
+        for (int pass = 0; pass <= last_pass; pass++) {
           WP.pass = pass;
           if (finish && pass == fin_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
-            static const bool fin_prof = getenv("RT_FINISH_PROF") != nullptr;  // development (RT_FINISH_PROF builds)
-            static unsigned long long* d_fin_log = nullptr;                    // never freed
-            if (fin_prof) {
-              if (!d_fin_log) HIPCHK(c, hipMalloc(&d_fin_log, (size_t)fgrid.x * 4 * 8 * 8));
-              HIPCHK(c, hipMemsetAsync(d_fin_log, 0, (size_t)fgrid.x * 4 * 8 * 8, sg[g]));
-              WP.K.wave_log = d_fin_log;
-            }
             if (fp->enable_bsdf) {
               if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
               else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
@@ -1476,38 +1454,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
             }
             HIPCHK(c, hipGetLastError());
-            if (fin_prof) {  // per-wave summary of this launch (syncs)
-              std::vector<unsigned long long> lg((size_t)fgrid.x * 4 * 8);
-              HIPCHK(c, hipStreamSynchronize(sg[g]));
-              HIPCHK(c, hipMemcpy(lg.data(), d_fin_log, lg.size() * 8, hipMemcpyDeviceToHost));
-              WP.K.wave_log = nullptr;
-              unsigned long long t0 = ~0ull;
-              std::vector<size_t> ws;
-              for (size_t i = 0; i < lg.size() / 8; i++)
-                if (lg[8 * i + 1]) { t0 = std::min(t0, lg[8 * i]); ws.push_back(i); }
-              std::sort(ws.begin(), ws.end(), [&](size_t a, size_t b) { return lg[8 * a + 1] > lg[8 * b + 1]; });
-              fprintf(stderr, "[rt] wf_finish group %d: %zu working waves\n", g, ws.size());
-              for (size_t k = 0; k < ws.size() && k < 6; k++) {
-                const unsigned long long* e = &lg[8 * ws[k]];
-                fprintf(stderr, "[rt]   wave end %.1f us (start %.1f): trace iters %llu, shade steps %llu, rays %llu, paths %llu, "
-                        "longest ray %llu iters\n", (e[1] - t0) / 100.0, (e[0] - t0) / 100.0, e[2], e[3], e[4], e[5],
-                        e[7]);
-              }
-              if (!ws.empty())
-                fprintf(stderr, "[rt]   wave ends: 50%% %.1f us, 90%% %.1f, 99%% %.1f\n", (lg[8 * ws[ws.size() / 2] + 1] - t0) / 100.0,
-                        (lg[8 * ws[ws.size() / 10] + 1] - t0) / 100.0, (lg[8 * ws[ws.size() / 100] + 1] - t0) / 100.0);
-            }
             break;
           }
-          // one stage: pass 0's camera paths are implicit (wf_trace / wf_shade generate them)
-          WP.cam_n = (stages == 1 && pass == 0) ? slots_g[g] : 0u;
-          if (pass < stages && stages > 1) {
-            WP.gen_f0 = pass * nfg / stages;
-            WP.gen_f1 = (pass + 1) * nfg / stages;
-            const unsigned int runs = ((unsigned)(WP.gen_f1 - WP.gen_f0) * (unsigned)c->n_valid + rtd::GEN_RUN - 1) / rtd::GEN_RUN;
-            hipLaunchKernelGGL(rtd::wf_gen, dim3(std::max(1u, std::min(runs, 8192u))), dim3(256), 0, sg[g], WP);
-            HIPCHK(c, hipGetLastError());
-          }
+          // pass 0's camera paths are implicit (wf_trace / wf_shade generate them)
+          WP.cam_n = pass == 0 ? slots_g[g] : 0u;
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));
@@ -1516,6 +1466,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           HIPCHK(c, hipEventRecord(t1, sg[g]));
           c->trace_events.push_back({t0, t1});
           c->trace_launches++;
+#ifdef RT_DEV
           if (debug_passes) {  // development aid: per-pass rays / visits / duration (syncs!)
             unsigned long long h[16];
             unsigned int q[2];
@@ -1571,6 +1522,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
                       us(ends[ends.size() * 99 / 100] - t0min), us(dmax), itmax, rmax);
             }
           }
+#endif
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
           if (fp->enable_bsdf)
@@ -1578,11 +1530,6 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           else
             hipLaunchKernelGGL(rtd::wf_shade<false>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
           HIPCHK(c, hipGetLastError());
-          if (!pix_split && g + 1 < G && pass == std::min(c->stagger, last_pass)) {
-            prev_stagger = take_event(c);
-            if (!prev_stagger) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
-            HIPCHK(c, hipEventRecord(prev_stagger, sg[g]));
-          }
         }
         // progressive blend in frame order: group g after group g-1 (pixel groups blend
         // disjoint pixels: no order between them)
@@ -1624,6 +1571,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       if (!c->batch_done) HIPCHK(c, hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming));
       HIPCHK(c, hipEventRecord(c->batch_done, c->stream));
     }
+    if (!LT->last_use) HIPCHK(c, hipEventCreateWithFlags(&LT->last_use, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(LT->last_use, c->stream));
     c->events.push_back({e0, e1});
     c->launches++;
     int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents);
@@ -1669,12 +1618,9 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->trace_ms = c->trace_ms;
   st->trace_iters = h[5];
   st->trace_iters_max = h[6];
-#ifdef RT_SHADE_PROF  // development variant: wave cycles per wf_shade phase (stats 16..21)
-  unsigned long long ph[6];
-  HIPCHK(c, hipMemcpy(ph, c->d_stats + 16, sizeof(ph), hipMemcpyDeviceToHost));
-  fprintf(stderr, "[shade-prof] sort %llu consume %llu bounce %llu store %llu append %llu flush %llu\n",
-          ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
-#endif
+  unsigned long long ps = 0;
+  HIPCHK(c, hipMemcpy(&ps, c->d_stats + 16, sizeof(ps), hipMemcpyDeviceToHost));
+  st->path_steps = ps;
   return RT_OK;
 }
 
@@ -1722,9 +1668,13 @@ static int cost_probe(rt_ctx* c, const rt_frame_params* fp, const float* rand_or
   c->cost_blocks = false;
   if (rc == RT_OK) {
     he = hipMemcpy(costs, c->d_tile_cost, n_bins * sizeof(uint64_t), hipMemcpyDeviceToHost);
-    if (he == hipSuccess) he = hipMemcpy(c->d_accum, saved, abytes, hipMemcpyDeviceToDevice);
     if (he != hipSuccess) rc = fail(c, RT_ERR_HIP, std::string("cost probe: ") + hipGetErrorString(he));
+  } else {
+    (void)rt_synchronize(c);  // whatever the failed call queued has finished with the accumulation
   }
+  // the accumulation is left as it was, on the error path too (the probe frames may have blended)
+  he = hipMemcpy(c->d_accum, saved, abytes, hipMemcpyDeviceToDevice);
+  if (he != hipSuccess && rc == RT_OK) rc = fail(c, RT_ERR_HIP, std::string("cost probe: ") + hipGetErrorString(he));
   (void)hipFree(saved);
   dfree(c->d_tile_cost);
   c->loop_num = loop;
@@ -1745,7 +1695,7 @@ int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   // dealt round-robin into the n_groups ranges a one-frame call splits the pixels into, so every
   // group gets an even share of the costly blocks, each in descending order
   int G = std::max(1, c->n_groups);
-  if (const char* e = getenv("RT_ORDER_RANGES")) G = std::max(1, atoi(e));  // (measurement)
+  if (const char* e = knob("RT_ORDER_RANGES")) G = std::max(1, atoi(e));  // (measurement)
   order.reserve(nb);
   for (int g = 0; g < G; g++)
     for (size_t k = (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);

@@ -5,7 +5,7 @@
 // pins ~170 VGPRs for the whole path.  Here a frame is a sequence of small kernels over
 // device-resident path state (one slot per pixel of this rank):
 //
-//   wf_gen     camera ray per pixel (RT:1520-1527)                  -> ray queue, active list
+//   wf_camera  camera ray direction and u*v per pixel (RT:1520-1527)  -> per-pixel table
 //   wf_trace   closest-hit / any-hit BVH traversal of every queued   -> (triangle, t) per ray
 //              ray, persistent grid with per-lane dynamic ray fetch
 //   wf_shade   per active path: apply the NEE result (RT:1389-1405),  -> next rays, next list
@@ -27,10 +27,7 @@
 
 namespace rtd {
 
-#ifndef RT_S5_PACK  // per-path seed/bounce/flags in 8 B instead of 16 (frame from the slot)
-#define RT_S5_PACK 1
-#endif
-// per-path flags (< 256: packed with the bounce when RT_S5_PACK)
+// per-path flags (< 256: packed with the bounce in s5.y)
 enum : uint32_t {
   PF_SHADOW = 1u,      // a shadow ray was traced for the current bounce (c_nee pending)
   PF_CMED = 2u,        // medium-emissive term pending (RT:1438)
@@ -46,11 +43,7 @@ struct WFState {
   float4* __restrict__ s2;   // evf.xyz, Le0.y
   float4* __restrict__ s3;   // cnee.xyz, Le0.z
   float4* __restrict__ s4;   // cmed.xyz, -
-#if RT_S5_PACK
   uint2* __restrict__ s5;    // wseed, bounce << 8 | flags (the frame is slot % frames: pixel-major)
-#else
-  uint4* __restrict__ s5;    // wseed, bounce, flags, frame
-#endif
   // rays in 24 B: {o.xyz, d.x} + {d.y, d.z} (continuation ra/rb, shadow sa/sb); 32 B as two
   // float4 cost the memory-bound shade 16 B of writes and 8 B of reads per path-bounce
   float4* __restrict__ ra;
@@ -77,10 +70,9 @@ struct WFParams {
   WFState S;
   int n_frames;  // frames in flight: slots = n_frames * K.n_work
   int pass;      // bounce pass: queue/active set pass&1 in, (pass+1)&1 out
-  int gen_f0, gen_f1;  // wf_gen: the frames [gen_f0, gen_f1) whose camera paths start this pass
   // implicit camera pass: when nonzero, this pass's ray queue and active list are the camera
   // paths of slots [0, cam_n) in slot order (entry i = slot i), generated where they are used
-  // (wf_trace refill, wf_shade) instead of being written by wf_gen and read back
+  // (wf_trace refill, wf_shade) instead of being written by a generation kernel and read back
   unsigned int cam_n;
 };
 
@@ -146,9 +138,6 @@ __global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
   }
 }
 
-#ifndef RT_SOBOL_TABLE
-#define RT_SOBOL_TABLE 1
-#endif
 // Per frame of a render call: sobolVec2(loopNum + 1, bounce) of RT:616-620 for bounces 0..3
 // (Sobol dims 0..7), so wf_shade reads one float2 instead of running two bit loops per bounce.
 // Also the blend weights of each frame, {1 / n, (n - 1) / n} with n = loopNum (RT:1552), the same
@@ -188,47 +177,6 @@ RTD f3 camera_ray(const KParams& P, const WFState& S, unsigned int slot, uint32_
   wseed = (uint32_t)(P.rand_origin[f] * 6.95857f * c.w);  // R5: rand_origin * 6.95857 * (u * v)
   frame = f;
   return xyz(c);
-}
-
-// ------------------------------------------------------------------------------- gen
-// Camera paths of frames [gen_f0, gen_f1) (RT:1520-1527), appended to the ray queue and active
-// list of this pass.  Frames start in stages (one stage per pass for the first passes): every
-// pass then mixes fresh camera paths with deeper bounces of earlier stages instead of the batch
-// ending in a long tail of nearly empty passes.  A block writes a contiguous run of GEN_RUN
-// slots behind one claim per list.
-constexpr unsigned int GEN_RUN = 256u * 8u;
-__global__ __launch_bounds__(256) void wf_gen(const WFParams W) {
-  const KParams& P = W.K;
-  const WFState& S = W.S;
-  const int in = W.pass & 1;
-  // item j of this stage = (work item j / nst, frame gen_f0 + j % nst): slots are pixel-major
-  const unsigned int nst = (unsigned)(W.gen_f1 - W.gen_f0), nfr = (unsigned)P.n_frames;
-  const unsigned int s1 = nst * P.n_work;
-  __shared__ unsigned int qbase, abase;
-  for (unsigned int run = blockIdx.x * GEN_RUN; run < s1; run += gridDim.x * GEN_RUN) {
-    const unsigned int n = min(GEN_RUN, s1 - run);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      qbase = atomicAdd(&S.cnt[in], n);
-      abase = atomicAdd(&S.cnt[2 + in], n);
-    }
-    __syncthreads();
-    for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
-      const unsigned int item = run + j, w = item / nst;
-      const unsigned int slot = w * nfr + (unsigned)W.gen_f0 + (item - w * nst);
-      uint32_t wseed, f;
-      const f3 d = camera_ray(P, S, slot, wseed, f);
-      put_ray(S.ra, S.rb, slot, P.pos[0], P.pos[1], P.pos[2], d.x, d.y, d.z);
-#if RT_S5_PACK
-      S.s5[slot] = make_uint2(wseed, PF_CONT | PF_CAMERA);
-      (void)f;
-#else
-      S.s5[slot] = make_uint4(wseed, 0u, PF_CONT | PF_CAMERA, f);
-#endif
-      S.queue[in][qbase + j] = (int)(slot << 1);
-      S.active[in][abase + j] = (int)slot;
-    }
-  }
 }
 
 // progressive blend of the frames in flight, in frame order (RT:1552).  Pixel-major slots put
@@ -271,18 +219,12 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
 // ----------------------------------------------------------------------------- trace
 // Persistent traversal: every lane pulls queued rays (one atomic per 64 rays per wave) and
 // runs the reference's near-first DFS (RT:338-390) with culling of subtrees that start beyond
-// the current closest hit.  Three wave schedules of the same per-lane steps (TraceMode):
-//   TM_IFIF  each iteration advances every busy lane by one internal node OR one triangle;
-//   TM_WW    while-while: internal nodes until every lane holds a leaf, then the leaf
-//            triangles, then the next pop (lanes doing the same kind of step stay together);
-//   TM_SPEC  while-while where a lane that reaches a leaf parks it and keeps descending until
-//            every lane has a parked leaf (Aila & Laine's speculative traversal).
-// All three visit a superset-free subset of the reference's nodes and return the same closest
-// hit (culling only drops subtrees whose entry distance exceeds the best hit so far).
-//   TM_DUAL  every lane keeps a traversal cursor and a triangle cursor and each iteration advances
-//            both (one triangle of the current leaf + one node step); a lane waits only when it
-//            reaches a second leaf before finishing the first; idle lanes refill every iteration.
-enum TraceMode { TM_IFIF = 0, TM_WW = 1, TM_SPEC = 2, TM_DUAL = 3 };
+// the current closest hit (culling only drops subtrees whose entry distance exceeds the best
+// hit so far, so the closest hit is the reference's).  The wave schedule is the dual cursor:
+// every lane keeps a traversal cursor and a triangle cursor and each iteration advances both (one
+// triangle of the current leaf + one node step); a lane waits only when it reaches a second leaf
+// before finishing the first, and idle lanes refill from the queue.  (Measured and removed: the
+// if-if schedule, while-while and Aila & Laine's speculative while-while)
 
 struct TraceLane {
   // ray as scalars (f3 members made SROA keep the lane in scratch memory)
@@ -344,12 +286,8 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
 }
 
 // one triangle (RT:241-299, R1); true when it becomes the closest hit
-// anyw (wave-uniform): every busy lane of the wave traces an any-hit (shadow) ray, whose best stays
-// +inf until the first hit ends it: the closest-hit bound and compare are skipped (scalar branch);
-// a hit at dist == best = +inf stays rejected by the tie rule, as for a closest-hit ray
 template <bool WIDE>
-RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc,
-                          bool anyw = false) {
+RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d());
@@ -360,30 +298,26 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   // fails RT:268 or the closest-hit test for certain.  NaN never rejects.
   const float qa = num * __builtin_amdgcn_rcpf(dn);
   if (qa < 0.0005f * (1.0f - 0x1p-16f)) return false;
-  if (!anyw && qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
+  if (qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
   const float t = num / dot(L.d(), ng);                                // RT:265
   const float dist = t - 0.00001f;
-  if (anyw) {
-    if (!(t >= 0.0005f && dist < INF)) return false;                   // RT:268 with best = +inf
-  } else if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) {
-    return false;                                                      // RT:268, RT:328/356
-  }
+  if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
   const f3 Pp = L.o() + L.d() * t;
   const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
   const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
   const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
   if (!((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0))) return false;
-  if (!anyw && WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
+  if (WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
   L.best = dist;
   L.besttri = i;
   L.bestt = t;
   return true;
 }
 template <bool WIDE>
-RTD bool tl_triangle(const KParams& P, TraceLane& L, int i, bool anyw = false) {
+RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   const uint32_t off = (uint32_t)i * 48u;
   const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
-  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc, anyw);
+  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc);
 }
 
 RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
@@ -576,7 +510,7 @@ RTD void tl_start(const KParams& P, TraceLane& L) {
   L.tri_i = L.tri_end = 0;
 }
 
-// one dual-cursor step of a lane's ray (see TM_DUAL): one triangle of the current leaf and one
+// one dual-cursor step of a lane's ray: one triangle of the current leaf and one
 // node; true when the ray is finished (stack empty and leaf done, or an any-hit found)
 template <bool WIDE>
 RTD bool tl_dual_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull) {
@@ -655,9 +589,6 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
   return tl_dual_calc(P, L, TS, cull, tl_dual_load(P, L, true));
 }
 
-#ifndef RT_TRACE_WPE
-#define RT_TRACE_WPE 1
-#endif
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
 #endif
@@ -672,18 +603,6 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
 #endif
-#ifndef RT_QUEUE_KIND_SEG  // wf_shade queues each block's shadow rays ahead of its continuations:
-                           // +0.4% C3, +1.0% C4 (tools/ab_proc.py, 3 rounds)
-#define RT_QUEUE_KIND_SEG 1
-#endif
-#ifndef RT_ZLO  // skip the all-zero Lo/Le0 rows of the path state (PF_ZLO)
-#define RT_ZLO 1
-#endif
-#ifndef RT_ANYHIT_WAVE  // waves whose busy lanes all trace shadow rays skip the closest-hit work:
-                        // measured -1.8% (C3) / -1.6% (C4) against the same queues without it (the
-                        // per-iteration ballot and scalar branches cost more than the VALU saved)
-#define RT_ANYHIT_WAVE 0
-#endif
 #ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed)
 #define RT_STATIC_FRAC 4
 #endif
@@ -693,8 +612,8 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
 // passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
 // a separate instantiation: the code alone cost the bulk's kernels 0.4%)
-template <bool COUNT, int MODE, bool WIDE, bool CAM, bool STATIC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == TM_DUAL ? RT_TRACE_WPE_DUAL : RT_TRACE_WPE)))
+template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
@@ -746,8 +665,7 @@ void wf_trace(const WFParams W) {
     pool_end = pool_next + static_per;
   }
   const int lane = (int)(threadIdx.x & 63);
-  int entry = 0, parked = 0;
-  bool haveParked = false;
+  int entry = 0;
   TraceLane L;
   L.ox = L.oy = L.oz = L.dx = L.dy = L.dz = L.ix = L.iy = L.iz = 0.0f;
   L.best = INF; L.bestt = 0.0f; L.besttri = -1;
@@ -759,17 +677,10 @@ void wf_trace(const WFParams W) {
   unsigned long long v_rays = 0, v_ovf = 0;  // COUNT: rays, overflow-column pushes
   unsigned long long v_q[6] = {0, 0, 0, 0, 0, 0};  // COUNT: node visits by breadth-first index
   const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
-#ifdef RT_TRACE_WAVELOG  // development: per-wave start/end/iterations/rays of the timed kernel (RT_DEBUG_PASSES)
-  const unsigned long long wl_t0 = wall_clock64();
-  unsigned long long wl_it = 0, wl_rays = 0;
-#endif
   const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
 
   while (true) {
     if (COUNT) v_iter++;
-#ifdef RT_TRACE_WAVELOG
-    wl_it++;
-#endif
     // ---- refill idle lanes from the wave's pool.  One counter serves the whole chip and a
     // single atomic address sustains only ~90 atomics/us, so the pool is claimed in big chunks
     // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
@@ -813,7 +724,6 @@ void wf_trace(const WFParams W) {
             L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
           }
           tl_start<WIDE>(P, L);
-          haveParked = false;
           busy = true;
         }
         pool_next += min((unsigned int)__popcll(idle), avail);
@@ -822,119 +732,40 @@ void wf_trace(const WFParams W) {
     if (!__any(busy)) break;
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
-    if (MODE == TM_DUAL) {
-      if (COUNT) { v_itN++; v_itT++; }
-      // every busy lane of the wave traces an any-hit (shadow) ray: best stays +inf until the hit
-      // that ends the ray, so culling drops nothing and the closest-hit bounds of the triangle test
-      // are moot; skipped behind scalar branches (wf_shade queues a block's shadow rays together)
-      const bool anyw = RT_ANYHIT_WAVE && __all(!busy || L.anyhit);
-      const bool cl = cull && !anyw;
-      if (busy) {
-        if (L.tri_i < L.tri_end) {
-          if (COUNT) { v_tri++; ray_steps++; }
-          if (tl_triangle<WIDE>(P, L, L.tri_i++, anyw) && L.anyhit) {
-            finished = true;
-            L.tri_end = L.tri_i;
-          }
+    if (COUNT) { v_itN++; v_itT++; }
+    if (busy) {
+      if (L.tri_i < L.tri_end) {
+        if (COUNT) { v_tri++; ray_steps++; }
+        if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+          finished = true;
+          L.tri_end = L.tri_i;
         }
-        if (!finished && L.haveCur) {
-          if (ref_is_leaf(L.cur)) {
-            if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
-              if (COUNT) { v_leaf++; v_park++; }
-              L.tri_i = leaf_first(L.cur);
-              L.tri_end = L.tri_i + leaf_count(L.cur);
-              L.haveCur = tl_pop(P, L, TS, cl);
-            }
-          } else {
-            if (COUNT) {
-              v_int++; ray_steps++;
-              if (WIDE) {  // node-visit histogram by breadth-first index (the LDS cache candidates)
-                v_q[0] += L.cur < 1; v_q[1] += L.cur < 5; v_q[2] += L.cur < 21;
-                v_q[3] += L.cur < 64; v_q[4] += L.cur < 85; v_q[5] += L.cur < 341;
-              }
-            }
-            const int sp0 = L.sp;
-            if (WIDE) tl_qnode(P, L, TS, cl);
-            else tl_node(P, L, TS, cl);
-            if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
-          }
-        }
-        if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
       }
-    } else if (MODE == TM_IFIF) {
-      if (busy) {
-        if (L.tri_i < L.tri_end) {
-          if (COUNT) v_tri++;
-          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) finished = true;
-        } else if (L.haveCur) {
-          if (ref_is_leaf(L.cur)) {
-            if (COUNT) v_leaf++;
+      if (!finished && L.haveCur) {
+        if (ref_is_leaf(L.cur)) {
+          if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
+            if (COUNT) { v_leaf++; v_park++; }
             L.tri_i = leaf_first(L.cur);
             L.tri_end = L.tri_i + leaf_count(L.cur);
-            L.haveCur = false;
-          } else {
-            if (COUNT) { v_int++; ray_steps++; }
-            if (WIDE) tl_qnode(P, L, TS, cull);
-            else tl_node(P, L, TS, cull);
+            L.haveCur = tl_pop(P, L, TS, cull);
           }
-        }
-        if (!finished && !L.haveCur && L.tri_i >= L.tri_end) {
-          L.haveCur = tl_pop(P, L, TS, cull);
-          if (!L.haveCur) finished = true;
-        }
-      }
-    } else {
-      // ---- internal nodes until every lane has a leaf (parked) or no work left
-      while (true) {
-        bool act;
-        if (MODE == TM_WW) {
-          act = busy && L.haveCur && !haveParked;
-          if (!__any(act)) break;
         } else {
-          if (__all(!busy || !L.haveCur || haveParked)) break;
-          act = busy && L.haveCur && !(haveParked && ref_is_leaf(L.cur));
-        }
-        if (COUNT) { v_iter++; v_itN++; }
-        if (act) {
-          if (ref_is_leaf(L.cur)) {
-            if (COUNT) v_park++;
-            parked = L.cur;
-            haveParked = true;
-            if (MODE == TM_WW) L.haveCur = false;
-            else L.haveCur = tl_pop(P, L, TS, cull);
-          } else {
-            if (COUNT) { v_int++; ray_steps++; }
-            if (WIDE) tl_qnode(P, L, TS, cull);
-            else tl_node(P, L, TS, cull);
+          if (COUNT) {
+            v_int++; ray_steps++;
+            if (WIDE) {  // node-visit histogram by breadth-first index (the LDS cache candidates)
+              v_q[0] += L.cur < 1; v_q[1] += L.cur < 5; v_q[2] += L.cur < 21;
+              v_q[3] += L.cur < 64; v_q[4] += L.cur < 85; v_q[5] += L.cur < 341;
+            }
           }
+          const int sp0 = L.sp;
+          if (WIDE) tl_qnode(P, L, TS, cull);
+          else tl_node(P, L, TS, cull);
+          if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
         }
       }
-      // ---- triangles of the parked leaf
-      if (haveParked) {
-        if (COUNT) v_leaf++;
-        L.tri_i = leaf_first(parked);
-        L.tri_end = L.tri_i + leaf_count(parked);
-        haveParked = false;
-      }
-      while (__any(L.tri_i < L.tri_end)) {
-        if (COUNT) { v_iter++; v_itT++; }
-        if (L.tri_i < L.tri_end) {
-          if (COUNT) { v_tri++; ray_steps++; }
-          if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
-            finished = true;
-            L.tri_end = L.tri_i;
-          }
-        }
-      }
-      if (busy && !finished && !L.haveCur) {
-        L.haveCur = tl_pop(P, L, TS, cull);
-        if (!L.haveCur) finished = true;
-      }
+      if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
     }
     if (busy && finished) {
-#ifdef RT_TRACE_WAVELOG
-      wl_rays++;
-#endif
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
       if (COUNT) {
         if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
@@ -949,15 +780,6 @@ void wf_trace(const WFParams W) {
       busy = false;
     }
   }
-#ifdef RT_TRACE_WAVELOG
-  if (!COUNT && P.wave_log) {
-    for (int off = 32; off > 0; off >>= 1) wl_rays += __shfl_xor(wl_rays, off);
-    if ((threadIdx.x & 63) == 0) {
-      unsigned long long* wv = P.wave_log + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
-      wv[0] = wl_t0; wv[1] = wall_clock64(); wv[2] = wl_it; wv[3] = wl_rays;
-    }
-  }
-#endif
   if (COUNT) {
     if (P.wave_log) {
       unsigned long long r = v_rays;
@@ -1010,49 +832,20 @@ void wf_trace(const WFParams W) {
                    // final build: 3 vs 2 +0.4%
 #define RT_SH_SUB 3
 #endif
-#ifndef RT_SH_KEY_MAT  // shade sort key: continuation hit + material (1) or hit only (0: +1.0%)
-#define RT_SH_KEY_MAT 0
-#endif
-constexpr int SH_KEYS = 8;  // 0: no continuation hit; 1 + material id % 7: continuation hit
-#ifndef RT_SH_SORT_MIN  // C3, pixel-major slots: 4 / 16 / 32 / 64 / 128 / 256 Mi -> -1.6 / -1.4 / -0.5 / 0 / +0.1 / +0.2%
-#define RT_SH_SORT_MIN (1u << 26)
-#endif
-constexpr unsigned int SH_SORT_MIN = RT_SH_SORT_MIN;  // active paths from which wf_shade sorts
-#ifndef RT_SH_SORT_REL
-#define RT_SH_SORT_REL 1  // N = 8 rank share +0.6%, N = 1 +0.1% over the absolute 64 Mi threshold
-#endif
+constexpr int SH_KEYS = 2;  // 0: no continuation hit (env / end of path); 1: a continuation hit
 
 // what a path's shade iteration will run: the cheap end-of-path / env branch or a bounce on
 // the hit material
 RTD int shade_key(const KParams& P, const WFState& S, int path) {
-#if RT_S5_PACK
   const uint32_t flags = S.s5[path].y & 0xffu;
-#else
-  const uint32_t flags = S.s5[path].z;
-#endif
   const int t = S.res[2 * path].x;
   if (!(flags & PF_CONT) || t < 0) return 0;
-#if RT_SH_KEY_MAT
-  return 1 + __float_as_int(P.trin[3 * t].w) % (SH_KEYS - 1);
-#else
   return 1;
-#endif
 }
 #ifndef RT_SHADE_WPE  // 4 waves/SIMD (<= 128 VGPRs, 12 B/lane spill): shade -8% vs the natural 3
 #define RT_SHADE_WPE 4
 #endif
 constexpr int SH_SUB = RT_SH_SUB;
-#ifdef RT_SHADE_PROF  // development variant: wave cycles per phase -> stats[16..21]
-#define SHP_DECL unsigned long long shp[6] = {0, 0, 0, 0, 0, 0}, shp_t = clock64();
-#define SHP_MARK(i) { const unsigned long long _n = clock64(); shp[i] += _n - shp_t; shp_t = _n; }
-#define SHP_PARAMS , unsigned long long (&shp)[6], unsigned long long& shp_t
-#define SHP_ARGS , shp, shp_t
-#else
-#define SHP_DECL
-#define SHP_MARK(i)
-#define SHP_PARAMS
-#define SHP_ARGS
-#endif
 
 // One path's shade step (the body of wf_shade, shared with wf_finish): consume the traced results
 // of the current bounce, sample the next one, write the state back and return the rays to queue.
@@ -1063,7 +856,7 @@ struct ShadeOut {
 };
 template <bool BSDF>
 RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
-                        unsigned long long& nsamples SHP_PARAMS) {
+                        unsigned long long& nsamples) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   bool doFinish = false, doBounce = false;
@@ -1079,19 +872,15 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   int mat = 0;
   if (live) {
     float4 cam_d = make_float4(0, 0, 0, 0);
-    if (camPass) {  // implicit camera pass: the state wf_gen would have written
+    if (camPass) {  // implicit camera pass: the state a camera path starts with
       uint32_t cseed, cframe;
       const f3 d = camera_ray(P, S, (unsigned)path, cseed, cframe);
       a5 = make_uint4(cseed, 0u, PF_CONT | PF_CAMERA, cframe);
       cam_d = make_float4(d.x, d.y, d.z, 0.0f);
     } else {
-#if RT_S5_PACK
       const uint2 p5 = S.s5[path];
       const unsigned int nfr = (unsigned int)W.n_frames;
       a5 = make_uint4(p5.x, p5.y >> 8, p5.y & 0xffu, (unsigned int)path % nfr);
-#else
-      a5 = S.s5[path];
-#endif
     }
     // every load of the path's state issues at once: camera paths exist only in pass 0 (a
     // uniform test), so no load waits for the flags; the flags still decide what is used
@@ -1099,9 +888,9 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     if (loadPrev) {
       a0 = S.s0[path]; a2 = S.s2[path];
       rsh = S.res[2 * path + 1];
-      // (RT_ZLO) a path whose Lo and Le0 are +0 (every path after a non-emissive camera hit, whose
+      // (PF_ZLO) a path whose Lo and Le0 are +0 (every path after a non-emissive camera hit, whose
       // NEE is still pending) skips the s1 row and, without a shadow ray, the s3 row
-      if (!RT_ZLO || !(a5.z & PF_ZLO)) {
+      if (!(a5.z & PF_ZLO)) {
         a1 = S.s1[path];
         a3 = S.s3[path];
       } else if (a5.z & PF_SHADOW) {
@@ -1210,7 +999,6 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
   }
 
-  SHP_MARK(1)
   // ------------------------------------------------------------- next bounce
   f3 cnee = splat(0.0f), cmed = splat(0.0f);
   uint32_t nflags = 0;
@@ -1238,14 +1026,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       nflags |= PF_SHADOW;
     }
     float sx, sy;
-#if RT_SOBOL_TABLE
     sobol_pair(P, frame, bounce, sx, sy);
-#else
-    int g = P.loop_num[frame] + 1;
-    g = g ^ (g >> 1);
-    sx = sobol_gray((int)bounce * 2, g);
-    sy = sobol_gray((int)bounce * 2 + 1, g);
-#endif
     const float cu = rand_(wseed), cv = rand_(wseed);
     sx += cu;
     if (sx > 1) sx -= 1;
@@ -1295,14 +1076,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
     // BSDF sample (RT:1408-1474)
     float sx, sy;
-#if RT_SOBOL_TABLE
     sobol_pair(P, frame, bounce, sx, sy);
-#else
-    int g = P.loop_num[frame] + 1;
-    g = g ^ (g >> 1);
-    sx = sobol_gray((int)bounce * 2, g);
-    sy = sobol_gray((int)bounce * 2 + 1, g);
-#endif
     const float cu = rand_(wseed), cv = rand_(wseed);
     sx += cu;
     if (sx > 1) sx -= 1;
@@ -1355,7 +1129,6 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
   }
 
-  SHP_MARK(2)
   // ----------------------------------------------------------- progressive blend
   if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
     S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
@@ -1365,7 +1138,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   // ------------------------------------------------------------ enqueue rays
   const bool keep = qShadow || qCont;
   if (keep) {
-    const bool zlo = RT_ZLO && (__float_as_uint(Lo.x) | __float_as_uint(Lo.y) | __float_as_uint(Lo.z) |
+    const bool zlo = (__float_as_uint(Lo.x) | __float_as_uint(Lo.y) | __float_as_uint(Lo.z) |
                                 __float_as_uint(Le0.x) | __float_as_uint(Le0.y) | __float_as_uint(Le0.z)) == 0u;
     if (zlo) nflags |= PF_ZLO;
     S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
@@ -1374,11 +1147,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     if (!zlo || qShadow) S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
     if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
     if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
-#if RT_S5_PACK
     S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
-#else
-    S.s5[path] = make_uint4(wseed, bounce, nflags, frame);
-#endif
     if (qCont) {
       put_ray(S.ra, S.rb, path, contO.x, contO.y, contO.z, contD.x, contD.y, contD.z);
     }
@@ -1386,7 +1155,6 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       put_ray(S.sa, S.sb, path, shO.x, shO.y, shO.z, shD.x, shD.y, shD.z);
     }
   }
-  SHP_MARK(3)
   return ShadeOut{qShadow, qCont};
 }
 
@@ -1404,11 +1172,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const int in = W.pass & 1, out = in ^ 1;
   const unsigned int na = W.cam_n ? W.cam_n : S.cnt[2 + in];
   const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
-  if (blockIdx.x == 0 && threadIdx.x == 0) S.cnt[4] = 0u;  // fetch counter of the next trace pass
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S.cnt[4] = 0u;  // fetch counter of the next trace pass
+    if (na) atomicAdd(&P.stats[16], (unsigned long long)na);  // path shade steps (rt_stats.path_steps)
+  }
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
-  SHP_DECL
   for (unsigned int base = blockIdx.x * (256u * SH_SUB); base < na; base += gridDim.x * (256u * SH_SUB)) {
   // ---- group the block's paths by what they will execute (block-local counting sort in LDS):
   // divergence between a continuation that missed (env lookup) and one that hit (a full BSDF
@@ -1421,13 +1191,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   if (threadIdx.x < SH_KEYS) lhist[threadIdx.x] = 0u;
   if (threadIdx.x == 0) lc[0] = lc[1] = lc[4] = 0u;
   __syncthreads();
-#if RT_SH_SORT_REL
   // sort only passes holding at least a quarter of the group's path slots (in practice pass 1,
   // whatever the per-rank pixel share)
   const bool sort_pass = W.pass != 0 && na >= max(1u << 22, (unsigned)W.n_frames * P.n_work / 4u);
-#else
-  const bool sort_pass = W.pass != 0 && na >= SH_SORT_MIN;
-#endif
   if (!sort_pass) {  // camera pass: hit/miss divergence is low already
 #pragma unroll
     for (int sub = 0; sub < SH_SUB; sub++) {
@@ -1457,32 +1223,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     if ((unsigned)sub * 256u + threadIdx.x < nblk) lsort[lofs[skey[sub]] + srank[sub]] = spath[sub];
   }
   __syncthreads();
-  SHP_MARK(0)
   for (int sub = 0; sub < SH_SUB; sub++) {
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
-    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples SHP_ARGS);
+    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
-#if RT_QUEUE_KIND_SEG
     // shadow rays from the front of the block's staging list, continuations from the back: the
     // block's queue run is [shadow rays][continuations], so a trace wave's claim is mostly one
-    // kind (RT_ANYHIT_WAVE)
+    // kind
     const unsigned int qs = wave_lds_append(&lc[0], qShadow ? 1u : 0u);
     const unsigned int qc = wave_lds_append(&lc[4], qCont ? 1u : 0u);
     if (qShadow) lq[qs] = (path << 1) | 1;
     if (qCont) lq[2 * 256 * SH_SUB - 1 - qc] = path << 1;
-#else
-    const unsigned int qs = wave_lds_append(&lc[0], (qShadow ? 1u : 0u) + (qCont ? 1u : 0u));
-    if (qShadow) lq[qs] = (path << 1) | 1;
-    if (qCont) lq[qs + (qShadow ? 1u : 0u)] = path << 1;
-#endif
     const unsigned int ai = wave_lds_append(&lc[1], keep ? 1u : 0u);
     if (keep) la[ai] = path;
-    SHP_MARK(4)
   }
   __syncthreads();
-#if RT_QUEUE_KIND_SEG
   if (threadIdx.x == 0) {
     lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[out], lc[0] + lc[4]) : 0u;
     lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
@@ -1490,22 +1247,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __syncthreads();
   for (unsigned int j = threadIdx.x; j < lc[0] + lc[4]; j += 256u)
     S.queue[out][lc[2] + j] = j < lc[0] ? lq[j] : lq[2 * 256 * SH_SUB - 1 - (j - lc[0])];
-#else
-  if (threadIdx.x == 0) {
-    lc[2] = lc[0] ? atomicAdd(&S.cnt[out], lc[0]) : 0u;
-    lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
-  }
-  __syncthreads();
-  for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue[out][lc[2] + j] = lq[j];
-#endif
   for (unsigned int j = threadIdx.x; j < lc[1]; j += 256u) S.active[out][lc[3] + j] = la[j];
   __syncthreads();
-  SHP_MARK(5)
   }
-#ifdef RT_SHADE_PROF
-  if ((threadIdx.x & 63) == 0)
-    for (int i = 0; i < 6; i++) atomicAdd(&P.stats[16 + i], shp[i]);
-#endif
   // per-wave counter flush
   for (int off = 32; off > 0; off >>= 1) {
     nrays += __shfl_xor(nrays, off);
@@ -1528,8 +1272,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // lane whose path ended takes the next one from the active list, and a wave runs shade steps in
 // batches of RT_FINISH_SHADE_MIN ready lanes (or when no lane is tracing), so a lane does not wait
 // for the wave's slowest ray of every bounce.  Same device functions in the same order per path:
-// the image and the ray count are unchanged.  (Per-wave profile, RT_FINISH_PROF: the finisher is
-// bound by latency at 2 waves/SIMD over ~80 paths per wave, not by single long rays.)
+// the image and the ray count are unchanged.  (A per-wave profile measured in round 2: the
+// finisher is bound by latency at 2 waves/SIMD over ~80 paths per wave, not by single long rays.)
 #ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
 #define RT_FINISH_SHADE_MIN 16
 #endif
@@ -1554,25 +1298,15 @@ void wf_finish(const WFParams W) {
   TS.ovf = (gu64*)(P.stack_ovf) + (blockIdx.x * TL_LANES + threadIdx.x);
   TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
-  unsigned long long nrays = 0, nsamples = 0;
-  SHP_DECL  // (RT_SHADE_PROF builds: shade_path's phase marks, not reported for the finisher)
+  unsigned long long nrays = 0, nsamples = 0, nsteps = 0;
   // lane state: no path / tracing the path's queued rays / rays done, waiting for its shade step
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
   TraceLane L;
   L.anyhit = false;
-#ifdef RT_FINISH_PROF  // development: per-wave timeline of the finisher -> P.wave_log (RT_FINISH_PROF env)
-  unsigned long long fp_it = 0, fp_sh = 0, fp_paths = 0;
-  unsigned int fp_ray = 0, fp_raymax = 0;
-  const unsigned long long fp_t0 = wall_clock64();
-#define FPROF(x) x
-#else
-#define FPROF(x)
-#endif
   // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation
   auto begin_rays = [&](bool sh, bool co) {
-    FPROF(fp_raymax = max(fp_raymax, fp_ray); fp_ray = 0;)
     contNext = sh && co;
     L.anyhit = sh;
     const float4 oa = sh ? S.sa[path] : S.ra[path];
@@ -1592,14 +1326,9 @@ void wf_finish(const WFParams W) {
       const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
       if (st == FS_IDLE && idx < na) {
         path = S.active[in][idx];
-#if RT_S5_PACK
         const uint32_t flags = S.s5[path].y & 0xffu;
-#else
-        const uint32_t flags = S.s5[path].z;
-#endif
         st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
         begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
-        FPROF(fp_paths++;)
       }
       drained = base + want >= na;
     }
@@ -1609,7 +1338,6 @@ void wf_finish(const WFParams W) {
     while (true) {
       const unsigned long long tr = __ballot(st == FS_TRACE);
       if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
-      FPROF(fp_it++; if (st == FS_TRACE) fp_ray++;)
       if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
         nrays++;
@@ -1618,10 +1346,10 @@ void wf_finish(const WFParams W) {
       }
     }
     if (__any(st == FS_SHADE)) {
-      FPROF(fp_sh++;)
       const bool sh = st == FS_SHADE;
-      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples SHP_ARGS);
+      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
       if (sh) {
+        nsteps++;
         if (o.qShadow || o.qCont) {
           st = FS_TRACE;
           begin_rays(o.qShadow, o.qCont);
@@ -1634,24 +1362,13 @@ void wf_finish(const WFParams W) {
   for (int off = 32; off > 0; off >>= 1) {
     nrays += __shfl_xor(nrays, off);
     nsamples += __shfl_xor(nsamples, off);
+    nsteps += __shfl_xor(nsteps, off);
   }
   if (lane == 0) {
     atomicAdd(&P.stats[0], nrays);
     atomicAdd(&P.stats[1], nsamples);
+    atomicAdd(&P.stats[16], nsteps);
   }
-#ifdef RT_FINISH_PROF
-  fp_raymax = max(fp_raymax, fp_ray);
-  for (int off = 32; off > 0; off >>= 1) {
-    fp_paths += __shfl_xor(fp_paths, off);
-    fp_raymax = max(fp_raymax, (unsigned)__shfl_xor((int)fp_raymax, off));
-  }
-  if (P.wave_log && lane == 0) {
-    unsigned long long* o = P.wave_log + 8 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
-    o[0] = fp_t0; o[1] = wall_clock64(); o[2] = fp_it; o[3] = fp_sh; o[4] = nrays; o[5] = fp_paths;
-    o[6] = 0; o[7] = fp_raymax;
-  }
-#endif
-#undef FPROF
 }
 
 }  // namespace rtd

@@ -80,7 +80,7 @@ class RtStats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("samples", C.c_uint64), ("internal_pops", C.c_uint64),
                 ("leaf_pops", C.c_uint64), ("tri_tests", C.c_uint64), ("launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("trace_launches", C.c_uint64), ("trace_ms", C.c_double),
-                ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64)]
+                ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64), ("path_steps", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -146,6 +146,14 @@ def lib(path: Optional[str] = None) -> C.CDLL:
     if _lib is None:
         _lib = _bind(C.CDLL(os.environ.get("RTAMD_LIB") or str(lib_path("librtamd.so"))))
     return _lib
+
+
+def dev_lib_path() -> str:
+    """lib/librtamd_dev.so: the same kernels built with -DRT_DEV, whose development settings
+    (test-only switches such as RT_CULL_EPS_SCALE, traversal-structure variants, A/B parameters)
+    are read from the environment.  Tests that exercise those load it explicitly; the release
+    librtamd.so reads no environment variable."""
+    return str(lib_path("librtamd_dev.so"))
 
 
 def _bind(L: C.CDLL) -> C.CDLL:

@@ -35,3 +35,13 @@ def gpu_renderer():
     r = Renderer(0)
     yield r
     r.close()
+
+
+@pytest.fixture(scope="session")
+def gpu_dev_renderer():
+    """A context of lib/librtamd_dev.so (-DRT_DEV): the development settings the test sets in the
+    environment (monkeypatch) reach the library; the release library ignores them."""
+    from rtamd.renderer import Renderer, dev_lib_path
+    r = Renderer(0, lib_path=dev_lib_path())
+    yield r
+    r.close()

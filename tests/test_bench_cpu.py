@@ -81,3 +81,47 @@ def test_bench_launcher_stops_the_other_ranks_when_one_fails():
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
     assert not any(ln.startswith("{") for ln in p.stdout.splitlines())
     assert time.time() - t0 < 90
+
+
+def test_trace_ray_bytes_follow_the_path_state_layout():
+    """bench.py's algorithmic bytes per secondary ray = queue entry + the WFState ray rows
+    (float4 {o.xyz, d.x} + float2 {d.y, d.z}) + the 8-B result (the constant had
+    kept the 32-B ray of an older layout)."""
+    import bench
+    src = (ROOT / "opengl-ray-tracing-framework_amd" / "csrc" / "hip" / "rt_wavefront.h").read_text()
+    assert "float4* __restrict__ ra;" in src and "float2* __restrict__ rb;" in src
+    assert "float4* __restrict__ sa;" in src and "float2* __restrict__ sb;" in src
+    assert "int2* __restrict__ res;" in src
+    assert bench.B_RAY_SECONDARY == 4 + (16 + 8) + 8
+    assert bench.B_RAY_CAMERA == 8
+
+
+def test_roofline_names_its_limiter_at_the_spec_clock():
+    """The roofline block prices wf_trace against HBM (the contract's roofline) and names the
+    limiter from the measured utilisations; VALU issue is computed at the 2.4 GHz spec clock over
+    the standalone launch time, so no field implies a clock or a bandwidth above the hardware's."""
+    import bench
+    st = {"rays": 2_000_000_000, "samples": 800_000_000, "trace_launches": 10, "path_steps": 1_000_000_000}
+    vis = {"rays": 1000, "internal_pops": 3000, "tri_tests": 3000}
+    prof = {"_file": "profiles/x.json", "kernels": {
+        "wf_trace": {"avg_launch_ms": 16.0, "avg_launch_ms_standalone": 12.0, "hbm_bytes_per_launch": 1.2e10,
+                     "SQ": {"SQ_INSTS_VALU": 6.6e9, "SQ_ACTIVE_INST_VALU": 6.7e9, "SQ_THREAD_CYCLES_VALU": 1.9e11}},
+        "wf_shade": {"avg_launch_ms": 13.0, "avg_launch_ms_standalone": 6.0, "hbm_bytes_per_launch": 3.0e10}}}
+    r = bench.roofline(st, vis, None, prof, 16.0)
+    assert r["bound"] == "hbm" and r["kernel"] == "wf_trace"
+    assert r["valu"]["spec_clock_ghz"] == 2.4
+    want = 6.6e9 * 2 / (1024 * 2.4e9 * 12e-3)
+    assert abs(r["valu"]["issue_frac_at_spec_clock"] - want) < 1e-4
+    assert r["limiter"] == max(r["utilisation"], key=r["utilisation"].get) == "valu_issue"
+    assert all(0 < v < 1 for v in r["utilisation"].values())
+    sh = r["kernels"]["wf_shade"]
+    assert sh["path_steps_per_launch"] == 100_000_000
+    assert 0 < sh["frac"] < sh["traffic_frac"] < 1
+    assert "clock_ghz" not in r["valu"]
+
+
+def test_cpu_baseline_records_the_host():
+    import bench
+    h = bench.host_cpus()
+    assert h["nproc"] >= 1 and 1 <= h["affinity"] <= h["nproc"]
+    assert "cpu_model" in h

@@ -303,7 +303,9 @@ def test_env_angle_changes_between_calls_match_oracle(gpu_renderer, env_maps):
     oracle's with that frame's angle, and the image and ray count match."""
     sd = cf.config_scene("C3")
     W, H = 96, 64
-    angles = [0.0, 0.25, 0.25, -0.4, 0.1, 0.0]
+    # two tables (one per angle in use): rebuilt on the call's stream after the last call that read
+    # the table; an angle still held by the other table is reused (0.1 after 0.0)
+    angles = [0.0, 0.25, 0.25, -0.4, 0.1, 0.0, 0.1, 0.1, -0.4, 0.0]
     ro = cf.rand_origins(len(angles))
     fps = [cf.frame_params(W, H, env_angle=a) for a in angles]
     frames = [cf.oracle_frame_params(fps[k], k + 1, ro[k]) for k in range(len(angles))]
@@ -320,3 +322,38 @@ def test_env_angle_changes_between_calls_match_oracle(gpu_renderer, env_maps):
     assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
     assert st["rays"] == cnt["rays"]
     r.set_pipeline(1)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_thousands_of_calls_without_synchronize(gpu_renderer, env_maps, depth):
+    """A front end that never calls rt_synchronize: more one-frame calls than the context keeps
+    timing-event pairs for (kMaxPendingEvents = 4096, rt_render.hip fold_events), with the pixel-
+    split groups (depth 1) or pipelined calls on alternating streams (depth 2), so the oldest
+    pairs are folded while later ones, on other streams, are still running.  Every call succeeds,
+    and the image and ray count equal one batched call of the same frames (itself bit-exact vs
+    the oracle elsewhere)."""
+    sd = cf.config_scene("C2")
+    W, H = 16, 16
+    n = 1100 if depth == 1 else 2100  # 4 / 2 trace-event pairs per call
+    fp = cf.frame_params(W, H)
+    ro = cf.rand_origins(n)
+    r = gpu_renderer
+    r.set_scene_soa(sd.soa, sd.nodes)
+    r.set_env(*env_maps)
+    r.resize(W, H)
+    r.reset_stats()
+    st = r.render(fp, ro)
+    ref = r.read_accum()
+    r.resize(W, H)
+    r.set_pipeline(depth)
+    r.reset_stats()
+    try:
+        for k in range(n):
+            r.render_async(fp, ro[k:k + 1])
+        st2 = r.stats()
+    finally:
+        r.set_pipeline(1)
+    assert r.loop_num == n
+    assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
+    assert st2["rays"] == st["rays"]
+    assert st2["launches"] == n

@@ -4,8 +4,9 @@ tests/cull_cases.py builds a scene where the reference's accepted closest hit (t
 several units before the entry of T's own box, and a wall between them is found first by the
 near-first traversal.  With the derived bound (cull_eps, rt_render.hip cull_bound_stats) the GPU
 image equals the oracle bit for bit; with the bound's eps term forced to 0
-(RT_CULL_EPS_SCALE=0, the round-1 margin) the GPU culls T's box and returns the wall: the test
-also checks that this failure shows, so it really exercises the hole.
+(RT_CULL_EPS_SCALE=0, the round-1 margin; a switch only lib/librtamd_dev.so reads) the GPU culls
+T's box and returns the wall: the test also checks that this failure shows, so it really
+exercises the hole.
 """
 import numpy as np
 import pytest
@@ -34,7 +35,7 @@ def _render_both(r, env, c, fp, W=8, H=8, n=2):
 
 
 @pytest.mark.parametrize("flags", [0, RT_FLAG_MEGAKERNEL], ids=["wavefront", "megakernel"])
-def test_culling_keeps_the_reference_hit(gpu_renderer, env_maps, monkeypatch, flags):
+def test_culling_keeps_the_reference_hit(gpu_renderer, gpu_dev_renderer, env_maps, monkeypatch, flags):
     c = old_margin_counterexample()
     fp = cull_frame_params(c)
     fp.flags = flags
@@ -42,6 +43,8 @@ def test_culling_keeps_the_reference_hit(gpu_renderer, env_maps, monkeypatch, fl
     assert st["rays"] == cnt["rays"]
     assert bit_mismatch(img, ref)[0] == 0.0
     monkeypatch.setenv("RT_CULL_EPS_SCALE", "0")
-    bad, _, _, _ = _render_both(gpu_renderer, env_maps, c, fp)
+    same, _, _, _ = _render_both(gpu_renderer, env_maps, c, fp)
+    assert bit_mismatch(same, ref)[0] == 0.0, "the release library must ignore RT_CULL_EPS_SCALE"
+    bad, _, _, _ = _render_both(gpu_dev_renderer, env_maps, c, fp)
     assert bit_mismatch(bad, ref)[0] > 0.5, "the round-1 margin should lose T on this scene"
     assert np.all(bad[..., 1] > bad[..., 0]), "with the round-1 margin the green wall wins"

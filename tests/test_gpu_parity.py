@@ -51,7 +51,7 @@ def test_encoded_aos_entry_point(gpu_renderer, env_maps):
     assert bit_mismatch(img, ref)[0] == 0.0
 
 
-def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_maps, monkeypatch):
+def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_maps):
     """Frames in flight are blended in frame order: 1 frame per wavefront (tiny path-state
     budget) and all frames at once give the same bits, and both equal the oracle."""
     sd = cf.config_scene("C3")
@@ -59,9 +59,11 @@ def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_m
     fp = cf.frame_params(W, H)
     ro, frames = frames_for(fp, 1, 3)
     ref, _ = oracle_render(sd, env_maps, W, H, frames)
-    monkeypatch.setenv("RT_MAX_SLOTS", str(W * H))  # -> one frame in flight
-    img1, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
-    monkeypatch.delenv("RT_MAX_SLOTS")
+    gpu_renderer.set_max_paths(W * H)  # -> one frame in flight
+    try:
+        img1, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    finally:
+        gpu_renderer.set_max_paths(0)  # the library default
     img3, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
     assert bit_mismatch(img1, ref)[0] == 0.0
     assert bit_mismatch(img3, ref)[0] == 0.0
@@ -69,7 +71,7 @@ def test_frames_in_flight_capacity_does_not_change_the_image(gpu_renderer, env_m
 
 @pytest.mark.parametrize("width,rebuild", [("4", "1"), ("4", "0"), ("2", "1")],
                          ids=["bvh4-rebuilt", "bvh4-reflevels", "bvh2"])
-def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monkeypatch, width, rebuild):
+def test_exact_distance_ties_follow_reference_order(gpu_dev_renderer, env_maps, monkeypatch, width, rebuild):
     """Two copies of the bunny at the same place with different materials: every hit on it is an
     exact distance tie between two triangles in different leaves.  The reference keeps the one
     its near-first DFS reaches first; the 4-wide traversal visits leaves in another order and
@@ -82,14 +84,14 @@ def test_exact_distance_ties_follow_reference_order(gpu_renderer, env_maps, monk
     ref, cnt = oracle_render(sd, env_maps, W, H, frames)
     monkeypatch.setenv("RT_BVH_WIDTH", width)
     monkeypatch.setenv("RT_REBUILD", rebuild)
-    img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    img, st = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
     assert st["rays"] == cnt["rays"]
     assert bit_mismatch(img, ref)[0] == 0.0
 
 
 @pytest.mark.parametrize("name", ["C3", "C5"])
-def test_reference_internal_levels_match_too(gpu_renderer, env_maps, monkeypatch, name):
-    """RT_REBUILD=0 collapses the reference's own internal nodes instead of the SAH levels rebuilt
+def test_reference_internal_levels_match_too(gpu_dev_renderer, env_maps, monkeypatch, name):
+    """RT_REBUILD=0 (lib/librtamd_dev.so) collapses the reference's own internal nodes instead of the SAH levels rebuilt
     over its leaves (rebuild_over_leaves): both reach exactly the leaves whose boxes the ray hits,
     so both images equal the oracle, and the rebuilt tree takes fewer node steps per ray."""
     from rtamd.renderer import RT_FLAG_COUNT_VISITS
@@ -101,21 +103,21 @@ def test_reference_internal_levels_match_too(gpu_renderer, env_maps, monkeypatch
     visits = {}
     for rebuild in ("0", "1"):
         monkeypatch.setenv("RT_REBUILD", rebuild)
-        img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+        img, st = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
         assert bit_mismatch(img, ref)[0] == 0.0, rebuild
         visits[rebuild] = st["internal_pops"] / st["rays"]
     assert visits["1"] < visits["0"], visits
 
 
-def test_binary_wavefront_traversal_matches(gpu_renderer, env_maps, monkeypatch):
-    """RT_BVH_WIDTH=2 keeps the wavefront trace on the binary tree (reference visit order)."""
+def test_binary_wavefront_traversal_matches(gpu_dev_renderer, env_maps, monkeypatch):
+    """RT_BVH_WIDTH=2 (lib/librtamd_dev.so) keeps the wavefront trace on the binary tree (reference visit order)."""
     sd = cf.config_scene("C3")
     W, H = 64, 36
     fp = cf.frame_params(W, H)
     ro, frames = frames_for(fp, 1, 2)
     ref, _ = oracle_render(sd, env_maps, W, H, frames)
     monkeypatch.setenv("RT_BVH_WIDTH", "2")
-    img, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    img, _ = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
     assert bit_mismatch(img, ref)[0] == 0.0
 
 
