@@ -28,6 +28,8 @@ def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     frac, _ = bit_mismatch(img, ref)
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert st["samples"] == cnt["samples"] == W * H * 2
+    if flags == 0:  # shade steps: one per path per pass, each after that path traced 1-2 rays
+        assert st["samples"] <= st["path_steps"] <= st["rays"], st
     assert frac == 0.0, f"{name}: {frac:.4%} of pixels differ from the oracle"
 
 

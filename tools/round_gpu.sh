@@ -4,7 +4,7 @@
 # driver's bench command (which reads that summary).  profiles/ comes back via gpurun_out/profiles.
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${TAG:-r02_C3}
+TAG=${TAG:-r03_C3}
 mkdir -p gpurun_out/profiles
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
