@@ -29,9 +29,12 @@
 #define GM_FN static inline
 #endif
 
-// RT_HW_MATH (measurement builds only, never the parity target): device code uses the
-// hardware / ocml transcendentals instead of the polynomials below, to price the bit-exact ones
-#if defined(RT_HW_MATH) && defined(__HIP_DEVICE_COMPILE__)
+// GM_LIBM (host code only: the oracle variant oracle/liboracle_libm.so): the transcendentals come
+// from the C library's fp32 functions (sinf, cosf, atan2f, asinf, expf, logf, powf) instead of the
+// polynomials below -- another implementation's builtin precision, to measure how much the image
+// depends on these definitions (tests/test_builtin_precision.py).  (A device-side variant with
+// the hardware v_sin/v_cos/v_exp/v_log was measured in round 2: no material speed-up, removed.)
+#if defined(GM_LIBM) && !defined(__HIP_DEVICE_COMPILE__)
 #define GM_HW 1
 #else
 #define GM_HW 0
@@ -69,7 +72,8 @@ GM_FN float exp2i_(int n) { return bitsf((uint32_t)(n + 127) << 23); }
 
 GM_FN void sincos_(float x, float* s_out, float* c_out) {
 #if GM_HW
-  __sincosf(x, s_out, c_out);
+  *s_out = sinf(x);
+  *c_out = cosf(x);
   return;
 #endif
   float j = rint_(x * GM_2OPI);
@@ -147,7 +151,7 @@ GM_FN float asin_(float x) {
 #define GM_LOG2EF 1.44269504088896341f
 GM_FN float exp_(float x) {
 #if GM_HW
-  return __expf(x);
+  return expf(x);
 #endif
   if (isnan_(x)) return x;
   if (x > 88.72283905206835f) return bitsf(0x7f800000u);
@@ -166,7 +170,7 @@ GM_FN float exp_(float x) {
 
 GM_FN float log_(float x) {
 #if GM_HW
-  return __logf(x);
+  return logf(x);
 #endif
   if (isnan_(x)) return x;
   if (x < 0.0f) return (x - x) / (x - x);
@@ -194,7 +198,7 @@ GM_FN float log_(float x) {
 // GLSL pow(x, y) (spec: exp2(y * log2(x)); undefined for x < 0).
 GM_FN float pow_(float x, float y) {
 #if GM_HW
-  return __powf(x, y);
+  return powf(x, y);
 #endif
   if (y == 0.0f) return 1.0f;
   if (x == 1.0f) return 1.0f;

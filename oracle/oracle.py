@@ -42,13 +42,14 @@ class OrcCounters(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-_lib = None
+_libs: dict = {}
 
 
-def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        p = ORACLE_DIR / "liboracle.so"
+def lib(variant: str = "") -> C.CDLL:
+    """liboracle.so, or liboracle_<variant>.so ("libm": the GLSL builtins from the C library's
+    fp32 functions instead of glsl_math.h's polynomials)."""
+    if variant not in _libs:
+        p = ORACLE_DIR / (f"liboracle_{variant}.so" if variant else "liboracle.so")
         if not p.exists():
             raise FileNotFoundError(f"{p} not built: make -C {ORACLE_DIR}")
         L = C.CDLL(str(p))
@@ -73,8 +74,8 @@ def lib() -> C.CDLL:
         L.orc_disney_eval.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_disney_sample.argtypes = [_f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, C.POINTER(C.c_int)]
         L.orc_display.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _fp(a: np.ndarray):
@@ -113,14 +114,14 @@ def frame_struct(params: dict) -> OrcFrame:
 
 def render(scene: OracleScene, frames: Sequence[dict], W: int, H: int, x0: int = 0, y0: int = 0,
            w: Optional[int] = None, h: Optional[int] = None, accum: Optional[np.ndarray] = None,
-           threads: int = 0):
+           threads: int = 0, variant: str = ""):
     """Render len(frames) progressive frames over the sub-rect; returns (accum (h,w,3), counters)."""
     w = W - x0 if w is None else w
     h = H - y0 if h is None else h
     acc = np.zeros((h, w, 3), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32).copy()
     fr = (OrcFrame * len(frames))(*[frame_struct(p) for p in frames])
     cnt = OrcCounters()
-    rc = lib().orc_render(C.byref(scene.c), fr, len(frames), W, H, x0, y0, w, h, _fp(acc), C.byref(cnt),
+    rc = lib(variant).orc_render(C.byref(scene.c), fr, len(frames), W, H, x0, y0, w, h, _fp(acc), C.byref(cnt),
                           threads or (os.cpu_count() or 1))
     if rc != 0:
         raise RuntimeError(f"orc_render failed: {rc}")
