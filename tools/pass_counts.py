@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Per-pass ray counts and durations of one-frame render calls (development aid, RT_DEV library).
+
+    RT_DEBUG_PASSES=1 RT_FINISH_PASS=99 python3 tools/pass_counts.py [--config C3] [--frames 1]
+
+Loads lib/librtamd_dev.so, renders warm-up frames, then one call of --frames frames with the
+per-pass report (stderr) of rt_render.hip's RT_DEBUG_PASSES."""
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "opengl-ray-tracing-framework_amd"))
+from rtamd import configs as cf  # noqa: E402
+from rtamd.renderer import Renderer, dev_lib_path  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C3")
+ap.add_argument("--frames", type=int, default=1)
+ap.add_argument("--count", action="store_true", help="RT_FLAG_COUNT_VISITS: steps-per-ray histograms per pass")
+a = ap.parse_args()
+cfg = cf.CONFIGS[a.config]
+W, H = cfg.width, cfg.height
+sd = cf.config_scene(a.config)
+r = Renderer(0, lib_path=dev_lib_path())
+r.set_scene_soa(sd.soa, sd.nodes)
+r.set_env(*cf.load_env())
+r.resize(W, H)
+from rtamd.renderer import RT_FLAG_COUNT_VISITS  # noqa: E402
+fp = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS if a.count else 0)
+ro = cf.rand_origins(8)
+print("---- measured call", file=sys.stderr, flush=True)
+st = r.render(fp, ro[:a.frames])
+print(st, flush=True)

@@ -28,7 +28,7 @@ for r in rows:
 
 def short(n):
     n = n.replace("rtd::", "").split("(")[0]
-    return n.replace("wf_trace<false, 3, true, false>", "trace").replace("wf_trace<false, 3, true, true>", "trace_cam") \
+    return n.replace("wf_trace<false, true, false, true>", "trace_s").replace("wf_trace<false, true, true, true>", "trace_cam_s").replace("wf_trace<false, true, false, false>", "trace").replace("wf_trace<false, true, true, false>", "trace_cam") \
             .replace("wf_shade<true>", "shade").replace("wf_shade<false>", "shade_brdf")
 
 
