@@ -9,9 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-ab}
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
-  tests/test_gpu_api.py tests/test_gpu_fullsize.py tests/test_gpu_materials.py tests/test_gpu_cull.py \
-  tests/test_interactive.py tests/test_display.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 HEAD_SO=opengl-ray-tracing-framework_amd/lib/exp/librtamd_head.so
 timeout -k 10 900 python3 tools/ab_proc.py --frames 1024 --whole --reps 2 --rounds 3 head=$HEAD_SO new=default > $O/ab.log 2>&1
