@@ -539,21 +539,31 @@ RTD bool tl_dual_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool
 
 // Fetch half of one dual step: the triangle's 48 B and the node's 112 B of lane ray L (when it
 // has them to do), before either test
+#ifndef RT_FINISH_TRI_PAIR  // the finisher fetches and tests two triangles of a leaf per step
+#define RT_FINISH_TRI_PAIR 1
+#endif
 struct DualLoad {
-  float4 A, B, Cc;
+  float4 A, B, Cc, A2, B2, C2;
   QLoad q;
-  bool doTri, doNode;
+  bool doTri, doTri2, doNode;
 };
 RTD DualLoad tl_dual_load(const KParams& P, const TraceLane& L, bool active) {
   DualLoad d;
   d.doTri = active && L.tri_i < L.tri_end;
   d.doNode = active && L.haveCur && !ref_is_leaf(L.cur);
-  d.A = d.B = d.Cc = make_float4(0, 0, 0, 0);
+  d.doTri2 = RT_FINISH_TRI_PAIR && d.doTri && L.tri_i + 1 < L.tri_end;
+  d.A = d.B = d.Cc = d.A2 = d.B2 = d.C2 = make_float4(0, 0, 0, 0);
   if (d.doTri) {
     const uint32_t off = (uint32_t)L.tri_i * 48u;
     d.A = ld<float4>(P.tri, off);
     d.B = ld<float4>(P.tri, off + 16u);
     d.Cc = ld<float4>(P.tri, off + 32u);
+  }
+  if (d.doTri2) {
+    const uint32_t off = (uint32_t)L.tri_i * 48u + 48u;
+    d.A2 = ld<float4>(P.tri, off);
+    d.B2 = ld<float4>(P.tri, off + 16u);
+    d.C2 = ld<float4>(P.tri, off + 32u);
   }
   if (d.doNode) d.q = tl_qnode_load(P, L);
   return d;
@@ -561,9 +571,13 @@ RTD DualLoad tl_dual_load(const KParams& P, const TraceLane& L, bool active) {
 // ... and the test half: the same steps as tl_dual_step (4-wide tree); true when the ray is done
 RTD bool tl_dual_calc(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull, const DualLoad& d) {
   bool finished = false;
-  if (d.doTri) {
+  if (d.doTri) {  // (the pair in index order, each test against the best after the one before)
     if (tl_triangle_calc<true>(P, L, L.tri_i, d.A, d.B, d.Cc) && L.anyhit) finished = true;
     L.tri_i++;
+    if (!finished && d.doTri2) {
+      if (tl_triangle_calc<true>(P, L, L.tri_i, d.A2, d.B2, d.C2) && L.anyhit) finished = true;
+      L.tri_i++;
+    }
     if (finished) L.tri_end = L.tri_i;
   }
   if (!finished && L.haveCur) {
