@@ -1374,8 +1374,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       static unsigned long long* d_wave_log = nullptr;  // never freed
       std::vector<unsigned long long> wave_log;
       if (debug_passes) {
-        if (!d_wave_log) HIPCHK(c, hipMalloc(&d_wave_log, (size_t)trace_grid * 4 * 4 * sizeof(unsigned long long)));
-        wave_log.resize((size_t)trace_grid * 4 * 4);
+        if (!d_wave_log) HIPCHK(c, hipMalloc(&d_wave_log, (size_t)trace_grid * 4 * 8 * sizeof(unsigned long long)));
+        wave_log.resize((size_t)trace_grid * 4 * 8);  // (the trace's records use the first half)
       }
 #else
       constexpr bool debug_passes = false;
@@ -1385,10 +1385,24 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       rtd::WFParams WG[rt_ctx::MAX_GROUPS];
       hipStream_t sg[rt_ctx::MAX_GROUPS];
       unsigned int slots_g[rt_ctx::MAX_GROUPS];
+      // pixel ranges of the groups (dev: RT_GROUP_SPLIT = group 0's share, the rest split evenly)
+      double split0 = -1.0;
+#ifdef RT_DEV
+      if (const char* e = knob("RT_GROUP_SPLIT")) split0 = atof(e);
+#endif
+      auto wbound = [&](int g) -> unsigned int {
+        if (g <= 0) return 0u;
+        if (g >= G) return (unsigned)c->n_valid;
+        if (split0 > 0.0 && G > 1) {
+          const size_t b0 = ((size_t)((double)c->n_valid * split0) + 63) / 64 * 64;
+          return (unsigned)std::min<size_t>((size_t)c->n_valid, b0 + ((size_t)c->n_valid - std::min<size_t>(b0, c->n_valid)) * (g - 1) / (G - 1));
+        }
+        return (unsigned)((size_t)c->n_valid * g / G);
+      };
       for (int g = 0; g < G; g++) {
         const int f0 = pix_split ? 0 : g * nf / G, f1 = pix_split ? nf : (g + 1) * nf / G;
-        const unsigned int w0 = pix_split ? (unsigned)((size_t)c->n_valid * g / G) : 0u;
-        const unsigned int w1 = pix_split ? (unsigned)((size_t)c->n_valid * (g + 1) / G) : (unsigned)c->n_valid;
+        const unsigned int w0 = pix_split ? wbound(g) : 0u;
+        const unsigned int w1 = pix_split ? wbound(g + 1) : (unsigned)c->n_valid;
         rtd::WFParams& WP = WG[g];
         WP.K = P;
         WP.K.loop_num = P.loop_num + f0;
@@ -1438,7 +1452,14 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         rtd::WFParams& WP = WG[g];
         HIPCHK(c, hipMemsetAsync(WP.S.cnt, 0, 64, sg[g]));
         // small groups (one frame per call) end their paths in wf_finish after pass finish_pass-1
-        const int fin_pass = (pipe && c->pipe_finish_pass >= 0) ? c->pipe_finish_pass : c->finish_pass;
+        int fin_pass = (pipe && c->pipe_finish_pass >= 0) ? c->pipe_finish_pass : c->finish_pass;
+#ifdef RT_DEV
+        {
+          char kn[32];
+          snprintf(kn, sizeof(kn), "RT_FINISH_PASS_G%d", g);
+          if (const char* e = knob(kn)) fin_pass = std::max(0, atoi(e));
+        }
+#endif
         const bool finish = !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
                             fin_pass >= 1 && fin_pass <= last_pass &&
                             ((fp->flags & RT_FLAG_FINISH) || slots_g[g] <= c->finish_slots);
@@ -1446,6 +1467,14 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           WP.pass = pass;
           if (finish && pass == fin_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
+#ifdef RT_DEV
+            hipEvent_t ft0 = nullptr, ft1 = nullptr;
+            if (debug_passes) {
+              HIPCHK(c, hipMemsetAsync(d_wave_log, 0, wave_log.size() * 8, sg[g]));
+              ft0 = take_event(c); ft1 = take_event(c);
+              HIPCHK(c, hipEventRecord(ft0, sg[g]));
+            }
+#endif
             if (fp->enable_bsdf) {
               if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
               else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
@@ -1454,6 +1483,46 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
             }
             HIPCHK(c, hipGetLastError());
+#ifdef RT_DEV
+            if (debug_passes) {  // development aid: the finisher's waves (syncs!)
+              HIPCHK(c, hipEventRecord(ft1, sg[g]));
+              HIPCHK(c, hipStreamSynchronize(sg[g]));
+              float ms = 0.0f;
+              HIPCHK(c, hipEventElapsedTime(&ms, ft0, ft1));
+              c->event_pool.push_back(ft0);
+              c->event_pool.push_back(ft1);
+              HIPCHK(c, hipMemcpy(wave_log.data(), d_wave_log, wave_log.size() * 8, hipMemcpyDeviceToHost));
+              struct FW { double t0, t1, sh_us; unsigned long long it, sh, paths; double at[3]; unsigned long long it_at[3]; };
+              std::vector<FW> fw;
+              double tmin = 1e300;
+              for (size_t w = 0; w < wave_log.size() / 8; w++) {
+                const unsigned long long* e = &wave_log[8 * w];
+                if (!e[1]) continue;
+                FW f{e[0] / 100.0, e[1] / 100.0, e[3] / 100.0, e[2] & 0xfffffull, (e[2] >> 20) & 0xfffffull, e[2] >> 40, {}, {}};
+                for (int q = 0; q < 3; q++) {
+                  f.at[q] = e[4 + q] ? (double)(e[4 + q] & 0xffffffffull) / 100.0 : -1.0;
+                  f.it_at[q] = e[4 + q] >> 32;
+                }
+                fw.push_back(f);
+                tmin = std::min(tmin, e[0] / 100.0);
+              }
+              std::sort(fw.begin(), fw.end(), [](const FW& a, const FW& b) { return a.t1 > b.t1; });
+              unsigned long long paths = 0;
+              for (const FW& f : fw) paths += f.paths;
+              fprintf(stderr, "[rt] group %d finisher from pass %d: %.3f ms, %zu waves, %llu paths; wave ends (us after the first "
+                      "start) 50%% %.1f 90%% %.1f 99%% %.1f 100%% %.1f\n", g, pass, ms, fw.size(), paths,
+                      fw.empty() ? 0.0 : fw[fw.size() / 2].t1 - tmin, fw.empty() ? 0.0 : fw[fw.size() / 10].t1 - tmin,
+                      fw.empty() ? 0.0 : fw[fw.size() / 100].t1 - tmin, fw.empty() ? 0.0 : fw[0].t1 - tmin);
+              for (size_t k = 0; k < std::min<size_t>(6, fw.size()); k++) {
+                const FW& f = fw[k];
+                fprintf(stderr, "[rt]   wave: start %.1f end %.1f us, %llu paths, %llu trace iterations (%.2f us each outside "
+                        "shade), %llu shade steps %.1f us (%.2f us each); <=16 / 4 / 1 busy lanes from %.0f / %.0f / %.0f us "
+                        "(iteration %llu / %llu / %llu)\n", f.t0 - tmin, f.t1 - tmin, f.paths, f.it,
+                        (f.t1 - f.t0 - f.sh_us) / (double)std::max(1ull, f.it), f.sh, f.sh_us, f.sh_us / (double)std::max(1ull, f.sh),
+                        f.at[0], f.at[1], f.at[2], f.it_at[0], f.it_at[1], f.it_at[2]);
+              }
+            }
+#endif
             break;
           }
           // pass 0's camera paths are implicit (wf_trace / wf_shade generate them)
@@ -1504,7 +1573,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               unsigned long long t0min = ~0ull, t1max = 0, t0max = 0, dmax = 0, itmax = 0, rmax = 0, cmax = 0;
               std::vector<unsigned long long> ends;
               double clk_sum = 0.0, wt_sum = 0.0;
-              for (size_t w = 0; w < wave_log.size() / 4; w++) {
+              for (size_t w = 0; w < wave_log.size() / 8; w++) {  // (trace_grid * 4 waves, 4 words each)
                 const unsigned long long* e = &wave_log[4 * w];
                 const unsigned long long its = e[2] & 0xfffffull, cyc = e[2] >> 20;
                 t0min = std::min(t0min, e[0]); t0max = std::max(t0max, e[0]); t1max = std::max(t1max, e[1]);
@@ -1697,8 +1766,14 @@ int rt_order_work(rt_ctx* c, const rt_frame_params* fp, const float* rand_origin
   int G = std::max(1, c->n_groups);
   if (const char* e = knob("RT_ORDER_RANGES")) G = std::max(1, atoi(e));  // (measurement)
   order.reserve(nb);
+  size_t head = 0;  // (measurement: RT_ORDER_HEAD = the costliest share first, the rest dealt into G-1 ranges)
+  if (const char* e = knob("RT_ORDER_HEAD")) {
+    head = std::min(nb, (size_t)((double)nb * atof(e)));
+    for (size_t k = 0; k < head; k++) order.push_back(sorted[k]);
+    G = std::max(1, G - 1);
+  }
   for (int g = 0; g < G; g++)
-    for (size_t k = (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);
+    for (size_t k = head + (size_t)g; k < nb; k += (size_t)G) order.push_back(sorted[k]);
   // permute the pixel list (xy then accumulation index) by whole blocks: a wave keeps its 8x8
   // block, and the blocks whose rays cost most are queued (and claimed) first
   std::vector<unsigned int> pix(2 * nv), out(2 * nv);

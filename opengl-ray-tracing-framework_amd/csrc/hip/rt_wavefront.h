@@ -1313,6 +1313,11 @@ void wf_finish(const WFParams W) {
   TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
   unsigned long long nrays = 0, nsamples = 0, nsteps = 0;
+#ifdef RT_FINISH_PROF  // (make variant HIPEXTRA=-DRT_FINISH_PROF) RT_DEBUG_PASSES: per-wave {t0, t1, trace iterations | shade steps << 20 | paths << 40, shade time}
+  const unsigned long long prof_t0 = wall_clock64();
+  unsigned long long prof_it = 0, prof_sh = 0, prof_paths = 0, prof_sh_t = 0;
+  unsigned long long prof_at[3] = {0, 0, 0}, prof_it_at[3] = {0, 0, 0};  // first time <= 16 / 4 / 1 lanes hold a path
+#endif
   // lane state: no path / tracing the path's queued rays / rays done, waiting for its shade step
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
@@ -1338,6 +1343,9 @@ void wf_finish(const WFParams W) {
       if (lane == 0) base = atomicAdd(&S.cnt[4], want);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
       const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
+#ifdef RT_FINISH_PROF
+      if (base < na) prof_paths += min(want, na - base);
+#endif
       if (st == FS_IDLE && idx < na) {
         path = S.active[in][idx];
         const uint32_t flags = S.s5[path].y & 0xffu;
@@ -1352,6 +1360,15 @@ void wf_finish(const WFParams W) {
     while (true) {
       const unsigned long long tr = __ballot(st == FS_TRACE);
       if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
+#ifdef RT_FINISH_PROF
+      prof_it++;
+      if (drained) {
+        const int busy = __popcll(__ballot(st != FS_IDLE));
+        const int lim[3] = {16, 4, 1};
+        for (int q = 0; q < 3; q++)
+          if (!prof_at[q] && busy <= lim[q]) { prof_at[q] = wall_clock64(); prof_it_at[q] = prof_it; }
+      }
+#endif
       if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
         nrays++;
@@ -1360,6 +1377,10 @@ void wf_finish(const WFParams W) {
       }
     }
     if (__any(st == FS_SHADE)) {
+#ifdef RT_FINISH_PROF
+      const unsigned long long ts = wall_clock64();
+      prof_sh++;
+#endif
       const bool sh = st == FS_SHADE;
       const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
       if (sh) {
@@ -1371,8 +1392,18 @@ void wf_finish(const WFParams W) {
           st = FS_IDLE;
         }
       }
+#ifdef RT_FINISH_PROF
+      prof_sh_t += wall_clock64() - ts;
+#endif
     }
   }
+#ifdef RT_FINISH_PROF
+  if (P.wave_log && lane == 0) {
+    unsigned long long* w = P.wave_log + 8 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+    w[0] = prof_t0; w[1] = wall_clock64(); w[2] = prof_it | (prof_sh << 20) | (prof_paths << 40); w[3] = prof_sh_t;
+    for (int q = 0; q < 3; q++) w[4 + q] = prof_at[q] ? ((prof_at[q] - prof_t0) | (prof_it_at[q] << 32)) : 0ull;
+  }
+#endif
   for (int off = 32; off > 0; off >>= 1) {
     nrays += __shfl_xor(nrays, off);
     nsamples += __shfl_xor(nsamples, off);

@@ -18,17 +18,21 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C3")
 ap.add_argument("--frames", type=int, default=1)
 ap.add_argument("--count", action="store_true", help="RT_FLAG_COUNT_VISITS: steps-per-ray histograms per pass")
+ap.add_argument("--lib", default=None, help="library (default lib/librtamd_dev.so)")
+ap.add_argument("--order", action="store_true", help="rt_order_work from one probe frame first (as bench.py does)")
 a = ap.parse_args()
 cfg = cf.CONFIGS[a.config]
 W, H = cfg.width, cfg.height
 sd = cf.config_scene(a.config)
-r = Renderer(0, lib_path=dev_lib_path())
+r = Renderer(0, lib_path=a.lib or dev_lib_path())
 r.set_scene_soa(sd.soa, sd.nodes)
 r.set_env(*cf.load_env())
 r.resize(W, H)
 from rtamd.renderer import RT_FLAG_COUNT_VISITS  # noqa: E402
 fp = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS if a.count else 0)
 ro = cf.rand_origins(8)
+if a.order:
+    r.order_work(cf.frame_params(W, H), ro[:1])
 print("---- measured call", file=sys.stderr, flush=True)
 st = r.render(fp, ro[:a.frames])
 print(st, flush=True)
