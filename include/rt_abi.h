@@ -150,7 +150,9 @@ int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_
 /* Longest-first work order (no GL counterpart: the rasteriser schedules fragments itself).  Renders
  * n_frames as a cost probe (as rt_tile_costs, state left unchanged), then reorders this ctx's pixel
  * list by whole 64-pixel blocks (an 8x8 block stays one wave) in descending cost, so the blocks
- * whose rays cost most are queued first and a pass's tail is the cheap blocks.  Results are
+ * whose rays cost most are queued first and a pass's tail is the cheap blocks; the costliest 5%
+ * become a pixel group of their own in one-frame calls (their long bounce chains reach the
+ * path-persistent finisher early, beside the rest's first passes).  Results are
  * unchanged (pixels are independent; the accumulation keeps its layout); rt_resize and
  * rt_set_tile_owners restore the natural order. */
 int rt_order_work(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames);

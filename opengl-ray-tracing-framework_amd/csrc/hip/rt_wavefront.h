@@ -1291,6 +1291,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
 #define RT_FINISH_SHADE_MIN 16
 #endif
+#ifndef RT_FINISH_HOLD_CONT  // the continuation ray fetched with the shadow ray, held in registers
+#define RT_FINISH_HOLD_CONT 1
+#endif
 #ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
 #define RT_FINISH_WPE 2
 #endif
@@ -1324,14 +1327,33 @@ void wf_finish(const WFParams W) {
   bool drained = false, contNext = false;
   TraceLane L;
   L.anyhit = false;
-  // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation
+  // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation, whose
+  // 24 B are fetched together with the shadow ray's and held until it starts (no load in the
+  // trace loop)
+  float4 ca = make_float4(0, 0, 0, 0);
+  float2 cb = make_float2(0, 0);
   auto begin_rays = [&](bool sh, bool co) {
     contNext = sh && co;
     L.anyhit = sh;
     const float4 oa = sh ? S.sa[path] : S.ra[path];
     const float2 ob = sh ? S.sb[path] : S.rb[path];
+    if (RT_FINISH_HOLD_CONT && contNext) {
+      ca = S.ra[path];
+      cb = S.rb[path];
+    }
     L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
     L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
+    tl_start<WIDE>(P, L);
+  };
+  auto begin_cont = [&]() {
+    if (!RT_FINISH_HOLD_CONT) {
+      begin_rays(false, true);
+      return;
+    }
+    contNext = false;
+    L.anyhit = false;
+    L.ox = ca.x; L.oy = ca.y; L.oz = ca.z;
+    L.dx = ca.w; L.dy = cb.x; L.dz = cb.y;
     tl_start<WIDE>(P, L);
   };
   while (true) {
@@ -1372,7 +1394,7 @@ void wf_finish(const WFParams W) {
       if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
         nrays++;
-        if (contNext) begin_rays(false, true);
+        if (contNext) begin_cont();
         else st = FS_SHADE;
       }
     }
