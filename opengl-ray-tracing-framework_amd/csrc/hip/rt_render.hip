@@ -1271,7 +1271,16 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     memcpy(&T.h[T.cap + n_traced], &rand_origin[k], 4);
     n_traced++;
   }
-  if (n_traced > 0) {
+  // small calls hand the pairs to wf_sobol as kernel arguments, which writes the table
+  rtd::InlineFrames IF;
+  memset(&IF, 0, sizeof(IF));
+  if (n_traced > 0 && n_traced <= RT_INLINE_FRAMES && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
+    IF.n_inline = n_traced;
+    for (int k = 0; k < n_traced; k++) {
+      IF.loop[k] = T.h[k];
+      memcpy(&IF.ro[k], &T.h[T.cap + k], 4);
+    }
+  } else if (n_traced > 0) {
     HIPCHK(c, hipMemcpyAsync(T.d, T.h, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, ps));
     HIPCHK(c, hipMemcpyAsync(T.d + T.cap, T.h + T.cap, (size_t)n_traced * sizeof(int), hipMemcpyHostToDevice, ps));
   }
@@ -1281,8 +1290,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   float2* d_sobol = reinterpret_cast<float2*>(T.d + 2 * T.cap);
   float2* d_blendw = reinterpret_cast<float2*>(T.d + 10 * T.cap);
   if (n_traced > 0 && !(fp->flags & RT_FLAG_MEGAKERNEL)) {
-    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, d_loop, d_sobol, d_blendw,
-                       n_traced);
+    hipLaunchKernelGGL(rtd::wf_sobol, dim3((4 * n_traced + 255) / 256), dim3(256), 0, ps, T.d,
+                       reinterpret_cast<float*>(T.d + T.cap), d_sobol, d_blendw, n_traced, IF);
     HIPCHK(c, hipGetLastError());
   }
   // NEE light table for this call's envAngle (SampleHdrLight): the table built for this angle, or
@@ -1470,6 +1479,9 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           if (finish && pass == fin_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
 #ifdef RT_DEV
+            if (const char* e = knob("RT_FINISH_LANES")) WP.K.fin_lanes = std::max(1, std::min(64, atoi(e)));
+#endif
+#ifdef RT_DEV
             hipEvent_t ft0 = nullptr, ft1 = nullptr;
             if (debug_passes) {
               HIPCHK(c, hipMemsetAsync(d_wave_log, 0, wave_log.size() * 8, sg[g]));
@@ -1510,7 +1522,15 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               }
               std::sort(fw.begin(), fw.end(), [](const FW& a, const FW& b) { return a.t1 > b.t1; });
               unsigned long long paths = 0;
-              for (const FW& f : fw) paths += f.paths;
+              double life = 0.0, tail16 = 0.0, tail4 = 0.0;
+              for (const FW& f : fw) {
+                paths += f.paths;
+                life += f.t1 - f.t0;
+                if (f.at[0] >= 0) tail16 += f.t1 - f.t0 - f.at[0];
+                if (f.at[1] >= 0) tail4 += f.t1 - f.t0 - f.at[1];
+              }
+              fprintf(stderr, "[rt] finisher wave time with <= 16 / <= 4 lanes holding a path (list drained): %.3f / %.3f of %.0f "
+                      "wave-us\n", tail16 / std::max(1.0, life), tail4 / std::max(1.0, life), life);
               fprintf(stderr, "[rt] group %d finisher from pass %d: %.3f ms, %zu waves, %llu paths; wave ends (us after the first "
                       "start) 50%% %.1f 90%% %.1f 99%% %.1f 100%% %.1f\n", g, pass, ms, fw.size(), paths,
                       fw.empty() ? 0.0 : fw[fw.size() / 2].t1 - tmin, fw.empty() ? 0.0 : fw[fw.size() / 10].t1 - tmin,
@@ -1532,7 +1552,17 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));
-          launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g], slots_g[g] <= c->finish_slots);
+          unsigned int tgrid = pass == 0 ? trace_grid0 : trace_grid1;
+#ifdef RT_DEV
+          {
+            char kn[32];
+            snprintf(kn, sizeof(kn), "RT_GRID_G%d", g);  // (measurement) trace blocks of group g
+            if (const char* e = knob(kn)) tgrid = std::max(1u, std::min(tgrid, (unsigned)atoi(e)));
+            snprintf(kn, sizeof(kn), "RT_GRID_G%d_P%d", g, pass);
+            if (const char* e = knob(kn)) tgrid = std::max(1u, std::min(tgrid, (unsigned)atoi(e)));
+          }
+#endif
+          launch_trace(c, count, dim3(tgrid), WP, sg[g], slots_g[g] <= c->finish_slots);
           HIPCHK(c, hipGetLastError());
           HIPCHK(c, hipEventRecord(t1, sg[g]));
           c->trace_events.push_back({t0, t1});

@@ -142,16 +142,33 @@ __global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
 // (Sobol dims 0..7), so wf_shade reads one float2 instead of running two bit loops per bounce.
 // Also the blend weights of each frame, {1 / n, (n - 1) / n} with n = loopNum (RT:1552), the same
 // operations wf_blend would run per pixel.
-__global__ __launch_bounds__(256) void wf_sobol(const int* __restrict__ loop_num, float2* __restrict__ out,
-                                                float2* __restrict__ blend_w, int n_frames) {
+// A call of at most RT_INLINE_FRAMES frames passes its (loopNum, randOrigin) pairs as kernel
+// arguments and this kernel writes them into the device frame table (no host-to-device copies in
+// a one-frame call's critical path); larger calls upload the table first (F.n_inline = 0).
+#ifndef RT_INLINE_FRAMES
+#define RT_INLINE_FRAMES 8
+#endif
+struct InlineFrames {
+  int n_inline;
+  int loop[RT_INLINE_FRAMES];
+  float ro[RT_INLINE_FRAMES];
+};
+__global__ __launch_bounds__(256) void wf_sobol(int* __restrict__ loop_num, float* __restrict__ rand_origin,
+                                                float2* __restrict__ out, float2* __restrict__ blend_w, int n_frames,
+                                                const InlineFrames F) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool inl = F.n_inline > 0;
   if (i < n_frames) {
-    const int loopNum = loop_num[i];
+    const int loopNum = inl ? F.loop[i] : loop_num[i];
+    if (inl) {
+      loop_num[i] = loopNum;
+      rand_origin[i] = F.ro[i];
+    }
     const float n = (float)loopNum;
     blend_w[i] = make_float2(1.0f / n, (float)(loopNum - 1) / n);
   }
   if (i >= n_frames * 4) return;
-  int g = loop_num[i >> 2] + 1;
+  int g = (inl ? F.loop[i >> 2] : loop_num[i >> 2]) + 1;
   g = g ^ (g >> 1);  // grayCode (RT:598-600)
   const int b = i & 3;
   out[i] = make_float2(sobol_gray(2 * b, g), sobol_gray(2 * b + 1, g));
@@ -1307,7 +1324,8 @@ void wf_finish(const WFParams W) {
   const unsigned int na = S.cnt[2 + in];
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
-  if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
+  const int fl = P.fin_lanes > 0 ? P.fin_lanes : 64;
+  if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * (unsigned)fl >= na) return;
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   TraceStack TS;
   TS.KL = P.lds_entries;
@@ -1358,7 +1376,7 @@ void wf_finish(const WFParams W) {
   };
   while (true) {
     // idle lanes take the next paths of the active list (one atomic per wave)
-    const unsigned long long idle = __ballot(st == FS_IDLE);
+    const unsigned long long idle = __ballot(st == FS_IDLE && lane < fl);
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
       unsigned int base = 0;
