@@ -623,6 +623,9 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
 #endif
+#ifndef RT_TRACE_PRIO
+#define RT_TRACE_PRIO 0
+#endif
 #ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s;
                        // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%;
                        // final build: 20 / 24 / 28 -> +0.3% / 0 / -0.9%
@@ -717,6 +720,15 @@ void wf_trace(const WFParams W) {
     // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
     // queue so the last rays still spread over all waves.
     const unsigned long long idle = __ballot(!busy);
+#if RT_TRACE_PRIO  // (measurement) fuller waves issue first in one-frame passes
+    if (STATIC) {
+      const int nb = 64 - __popcll(idle);
+      if (nb > RT_TRACE_PRIO) __builtin_amdgcn_s_setprio(3);
+      else if (nb > RT_TRACE_PRIO / 2) __builtin_amdgcn_s_setprio(2);
+      else if (nb > RT_TRACE_PRIO / 4) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
@@ -1311,6 +1323,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_HOLD_CONT  // the continuation ray fetched with the shadow ray, held in registers
 #define RT_FINISH_HOLD_CONT 1
 #endif
+#ifndef RT_FINISH_PRIO  // wave priority 3 / 2 / 1 / 0 above this many / half / a quarter / fewer lanes holding a
+// path: the finisher is issue-bound while its waves share the SIMDs, and half of its wave time is
+// waves with <= 16 paths left, so full waves (the long bounce chains of costly pixels) go first.
+// C3 1080p single frames -3.5% (32: -3.2%; two levels at 16 / 8 / 32: -2.8 / -2.5 / -2.1%)
+#define RT_FINISH_PRIO 16
+#endif
 #ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
 #define RT_FINISH_WPE 2
 #endif
@@ -1395,6 +1413,13 @@ void wf_finish(const WFParams W) {
       drained = base + want >= na;
     }
     if (!__any(st != FS_IDLE)) break;
+    {  // fuller waves issue first (s_setprio by the lanes holding a path; see RT_FINISH_PRIO)
+      const int busy = __popcll(__ballot(st != FS_IDLE));
+      if (busy > RT_FINISH_PRIO) __builtin_amdgcn_s_setprio(3);
+      else if (busy > RT_FINISH_PRIO / 2) __builtin_amdgcn_s_setprio(2);
+      else if (busy > RT_FINISH_PRIO / 4) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     // trace until enough lanes wait for their shade step (or none is tracing): a lane never waits
     // for the wave's slowest ray of every bounce, only for a batch of shade steps
     while (true) {
