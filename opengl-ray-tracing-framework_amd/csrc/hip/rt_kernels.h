@@ -62,7 +62,6 @@ struct KParams {
   unsigned int* __restrict__ counter;
   unsigned long long* __restrict__ stats;  // rays, samples, internal, leaf, tri
   unsigned long long* __restrict__ wave_log;  // debug (RT_DEBUG_PASSES): per trace wave {t0, t1, iters, rays}
-  int fin_lanes;  // (measurement) lanes per wf_finish wave that take paths; 0 = 64
 };
 
 struct Visits {

@@ -1436,6 +1436,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
+        // (not for frame groups of one frame each: their blends must run in frame order)
+        WP.fuse_blend = (!pipe && WP.n_frames == 1 && (pix_split || G == 1) && !count) ? 1 : 0;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
         sg[g] = pipe ? ps : g == 0 ? c->stream : c->aux[g];
       }
@@ -1478,9 +1480,6 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           WP.pass = pass;
           if (finish && pass == fin_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
-#ifdef RT_DEV
-            if (const char* e = knob("RT_FINISH_LANES")) WP.K.fin_lanes = std::max(1, std::min(64, atoi(e)));
-#endif
 #ifdef RT_DEV
             hipEvent_t ft0 = nullptr, ft1 = nullptr;
             if (debug_passes) {
@@ -1552,17 +1551,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           hipEvent_t t0 = take_event(c), t1 = take_event(c);
           if (!t0 || !t1) return fail(c, RT_ERR_HIP, "hipEventCreate failed");
           HIPCHK(c, hipEventRecord(t0, sg[g]));
-          unsigned int tgrid = pass == 0 ? trace_grid0 : trace_grid1;
-#ifdef RT_DEV
-          {
-            char kn[32];
-            snprintf(kn, sizeof(kn), "RT_GRID_G%d", g);  // (measurement) trace blocks of group g
-            if (const char* e = knob(kn)) tgrid = std::max(1u, std::min(tgrid, (unsigned)atoi(e)));
-            snprintf(kn, sizeof(kn), "RT_GRID_G%d_P%d", g, pass);
-            if (const char* e = knob(kn)) tgrid = std::max(1u, std::min(tgrid, (unsigned)atoi(e)));
-          }
-#endif
-          launch_trace(c, count, dim3(tgrid), WP, sg[g], slots_g[g] <= c->finish_slots);
+          launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g], slots_g[g] <= c->finish_slots);
           HIPCHK(c, hipGetLastError());
           HIPCHK(c, hipEventRecord(t1, sg[g]));
           c->trace_events.push_back({t0, t1});
@@ -1626,10 +1615,13 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
 #endif
           const unsigned int shade_grid = std::max(
               1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * rtd::SH_SUB - 1) / (256u * rtd::SH_SUB)));
-          if (fp->enable_bsdf)
-            hipLaunchKernelGGL(rtd::wf_shade<true>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
-          else
-            hipLaunchKernelGGL(rtd::wf_shade<false>, dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          if (fp->enable_bsdf) {
+            if (WP.fuse_blend) hipLaunchKernelGGL((rtd::wf_shade<true, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+            else hipLaunchKernelGGL((rtd::wf_shade<true, false>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          } else {
+            if (WP.fuse_blend) hipLaunchKernelGGL((rtd::wf_shade<false, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+            else hipLaunchKernelGGL((rtd::wf_shade<false, false>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+          }
           HIPCHK(c, hipGetLastError());
         }
         // progressive blend in frame order: group g after group g-1 (pixel groups blend
@@ -1643,8 +1635,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           c->event_pool.push_back(e_entry);  // reusable once the wait is enqueued
           e_entry = nullptr;
         }
-        hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WP);
-        HIPCHK(c, hipGetLastError());
+        if (!WP.fuse_blend) {
+          hipLaunchKernelGGL(rtd::wf_blend, dim3(blend_grid), dim3(256), 0, sg[g], WP);
+          HIPCHK(c, hipGetLastError());
+        }
         if (!pix_split && g + 1 < G) {
           prev_blend = take_event(c);
           if (!prev_blend) return fail(c, RT_ERR_HIP, "hipEventCreate failed");

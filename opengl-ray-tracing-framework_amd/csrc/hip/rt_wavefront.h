@@ -74,6 +74,10 @@ struct WFParams {
   // paths of slots [0, cam_n) in slot order (entry i = slot i), generated where they are used
   // (wf_trace refill, wf_shade) instead of being written by a generation kernel and read back
   unsigned int cam_n;
+  // one frame per path-state set and nothing in flight before it (unpipelined calls of one frame
+  // per group): a finishing path blends into the accumulation itself (wf_blend's operations,
+  // RT:1552) instead of writing fin for a wf_blend launch after the last pass
+  int fuse_blend;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -623,9 +627,6 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
 #endif
-#ifndef RT_TRACE_PRIO
-#define RT_TRACE_PRIO 0
-#endif
 #ifndef RT_REFILL_MIN  // measured on C3 (tools/exp_ab.sh): 1 -> 5399, 8 -> 5755, 16 -> 5839, 32 -> 5645 Mrays/s;
                        // on the rebuilt tree with 512-ray claims: 8 / 16 / 24 / 32 -> -2.8% / 0 / +0.6% / -1.0%;
                        // final build: 20 / 24 / 28 -> +0.3% / 0 / -0.9%
@@ -720,15 +721,6 @@ void wf_trace(const WFParams W) {
     // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
     // queue so the last rays still spread over all waves.
     const unsigned long long idle = __ballot(!busy);
-#if RT_TRACE_PRIO  // (measurement) fuller waves issue first in one-frame passes
-    if (STATIC) {
-      const int nb = 64 - __popcll(idle);
-      if (nb > RT_TRACE_PRIO) __builtin_amdgcn_s_setprio(3);
-      else if (nb > RT_TRACE_PRIO / 2) __builtin_amdgcn_s_setprio(2);
-      else if (nb > RT_TRACE_PRIO / 4) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-#endif
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
@@ -897,7 +889,7 @@ constexpr int SH_SUB = RT_SH_SUB;
 struct ShadeOut {
   bool qShadow, qCont;
 };
-template <bool BSDF>
+template <bool BSDF, bool FUSE = false>  // FUSE: W.fuse_blend is honoured (one-frame pixel groups)
 RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
                         unsigned long long& nsamples) {
   const KParams& P = W.K;
@@ -1174,7 +1166,15 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
 
   // ----------------------------------------------------------- progressive blend
   if (doFinish) {  // curColor of RT:1549; blended by wf_blend in frame order
-    S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
+    if (FUSE && W.fuse_blend) {  // one frame: the blend of this pixel, here (same operations as wf_blend)
+      const unsigned int ai = S.pix_acc[path];
+      const float4 h = P.accum[ai];
+      const float2 bw = P.blend_w[frame];  // {1 / n, (n - 1) / n} (wf_sobol)
+      const f3 acc = bw.x * fin + bw.y * mk3(h.x, h.y, h.z);
+      P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+    } else {
+      S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
+    }
     nsamples++;
   }
 
@@ -1203,7 +1203,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
 
 // BSDF: enableBSDF (RT:1369 Disney integrator) or the BRDF integrator (RT:1290), one
 // instantiation each so neither carries the other's registers
-template <bool BSDF>
+template <bool BSDF, bool FUSE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
   __shared__ int lq[2 * 256 * SH_SUB];
   __shared__ int la[256 * SH_SUB];
@@ -1270,7 +1270,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
-    const ShadeOut so = shade_path<BSDF>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
+    const ShadeOut so = shade_path<BSDF, FUSE>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
     // shadow rays from the front of the block's staging list, continuations from the back: the
     // block's queue run is [shadow rays][continuations], so a trace wave's claim is mostly one
@@ -1342,8 +1342,7 @@ void wf_finish(const WFParams W) {
   const unsigned int na = S.cnt[2 + in];
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
-  const int fl = P.fin_lanes > 0 ? P.fin_lanes : 64;
-  if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * (unsigned)fl >= na) return;
+  if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   TraceStack TS;
   TS.KL = P.lds_entries;
@@ -1394,7 +1393,7 @@ void wf_finish(const WFParams W) {
   };
   while (true) {
     // idle lanes take the next paths of the active list (one atomic per wave)
-    const unsigned long long idle = __ballot(st == FS_IDLE && lane < fl);
+    const unsigned long long idle = __ballot(st == FS_IDLE);
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
       unsigned int base = 0;
@@ -1447,7 +1446,7 @@ void wf_finish(const WFParams W) {
       prof_sh++;
 #endif
       const bool sh = st == FS_SHADE;
-      const ShadeOut o = shade_path<BSDF>(W, E, path, sh, false, true, nsamples);
+      const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, nsamples);
       if (sh) {
         nsteps++;
         if (o.qShadow || o.qCont) {

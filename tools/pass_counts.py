@@ -19,6 +19,7 @@ ap.add_argument("--config", default="C3")
 ap.add_argument("--frames", type=int, default=1)
 ap.add_argument("--count", action="store_true", help="RT_FLAG_COUNT_VISITS: steps-per-ray histograms per pass")
 ap.add_argument("--lib", default=None, help="library (default lib/librtamd_dev.so)")
+ap.add_argument("--warm", type=int, default=0, help="one-frame calls before the measured one (timelines)")
 ap.add_argument("--order", action="store_true", help="rt_order_work from one probe frame first (as bench.py does)")
 a = ap.parse_args()
 cfg = cf.CONFIGS[a.config]
@@ -33,6 +34,8 @@ fp = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS if a.count else 0)
 ro = cf.rand_origins(8)
 if a.order:
     r.order_work(cf.frame_params(W, H), ro[:1])
+for k in range(a.warm):
+    r.render(cf.frame_params(W, H), ro[k % 8:k % 8 + 1])
 print("---- measured call", file=sys.stderr, flush=True)
 st = r.render(fp, ro[:a.frames])
 print(st, flush=True)

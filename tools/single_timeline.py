@@ -29,7 +29,8 @@ for r in rows:
 def short(n):
     n = n.replace("rtd::", "").split("(")[0]
     return n.replace("wf_trace<false, true, false, true>", "trace_s").replace("wf_trace<false, true, true, true>", "trace_cam_s").replace("wf_trace<false, true, false, false>", "trace").replace("wf_trace<false, true, true, false>", "trace_cam") \
-            .replace("wf_shade<true>", "shade").replace("wf_shade<false>", "shade_brdf")
+            .replace("wf_shade<true, true>", "shade_fb").replace("wf_shade<true, false>", "shade") \
+            .replace("wf_shade<false, true>", "shade_brdf_fb").replace("wf_shade<false, false>", "shade_brdf")
 
 
 spans = []
