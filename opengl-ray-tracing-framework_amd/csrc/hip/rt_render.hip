@@ -685,6 +685,7 @@ void update_frames_cap(rt_ctx* c, size_t nv) {
 // Path-state buffers of the wavefront path: `paths` slots for each of the n_groups frame
 // groups, carved from one allocation (192 B per slot + counters).  RT_ERR_NOMEM when HBM
 // cannot hold them (the caller then runs fewer frames at a time).
+static_assert(rt_ctx::MAX_GROUPS <= 4, "rtd::GroupCounters holds 4 groups' counters");
 int alloc_wavefront(rt_ctx* c, size_t paths) {
   if (c->wf_mem && c->wf_paths >= paths) return RT_OK;
   if (c->wf_mem) {  // grow: earlier launches on the streams may still read the old state
@@ -1447,8 +1448,12 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       WC.S.pix_xy = c->wf.pix_xy;
       WC.S.pix_acc = c->wf.pix_acc;
       WC.S.cam = WG[0].S.cam;
+      rtd::GroupCounters Z;
+      memset(&Z, 0, sizeof(Z));
+      Z.n = G;
+      for (int g = 0; g < G; g++) Z.cnt[g] = WG[g].S.cnt;
       hipLaunchKernelGGL(rtd::wf_camera, dim3(std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256))),
-                         dim3(256), 0, ps, WC);
+                         dim3(256), 0, ps, WC, Z);
       HIPCHK(c, hipGetLastError());
       // aux streams start after everything already queued on the caller's stream
       if (G > 1) {
@@ -1462,8 +1467,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const unsigned int blend_grid = std::max(1u, std::min<unsigned int>(2048u, ((unsigned)c->n_valid + 255) / 256));
       hipEvent_t prev_blend = nullptr;
       for (int g = 0; g < G; g++) {
-        rtd::WFParams& WP = WG[g];
-        HIPCHK(c, hipMemsetAsync(WP.S.cnt, 0, 64, sg[g]));
+        rtd::WFParams& WP = WG[g];  // (its pass counters were zeroed by wf_camera)
         // small groups (one frame per call) end their paths in wf_finish after pass finish_pass-1
         int fin_pass = (pipe && c->pipe_finish_pass >= 0) ? c->pipe_finish_pass : c->finish_pass;
 #ifdef RT_DEV

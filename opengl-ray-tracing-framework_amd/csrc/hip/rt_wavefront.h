@@ -125,10 +125,16 @@ RTD unsigned int wave_lds_append(unsigned int* lcount, unsigned int n) {
 }
 
 // Per work item of this rank: the camera ray direction and u*v of its pixel (RT:1520-1527),
-// written once per render call; every frame's camera ray of that pixel reads it.
-__global__ __launch_bounds__(256) void wf_camera(const WFParams W) {
+// written once per render call; every frame's camera ray of that pixel reads it.  Block 0 also
+// zeroes the batch's groups' pass counters (16 words each: no memset ahead of each group's passes).
+struct GroupCounters {
+  unsigned int* cnt[4];
+  int n;
+};
+__global__ __launch_bounds__(256) void wf_camera(const WFParams W, const GroupCounters Z) {
   const KParams& P = W.K;
   const WFState& S = W.S;
+  if (blockIdx.x == 0 && threadIdx.x < 16u * (unsigned)Z.n) Z.cnt[threadIdx.x >> 4][threadIdx.x & 15u] = 0u;
   const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
   const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
   const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
