@@ -1760,6 +1760,10 @@ static int cost_probe(rt_ctx* c, const rt_frame_params* fp, const float* rand_or
   }
   rt_frame_params q = *fp;
   q.flags = (q.flags | RT_FLAG_COUNT_VISITS) & ~RT_FLAG_MEGAKERNEL;
+  // rt_order_work ranks blocks by their camera rays alone: the camera pass is the same in every
+  // frame (R6), so the order does not depend on the probe frame's random bounces (C3 1080p, 10
+  // probe frames: single frames 2.85-2.89 ms with it, 2.85-3.10 ms from whole-path costs)
+  if (blocks) q.max_bounce = 0;
   c->tile_cost_on = true;
   c->cost_blocks = blocks;
   rc = rt_render(c, &q, rand_origin, n_frames, nullptr);
