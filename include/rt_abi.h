@@ -147,8 +147,9 @@ int rt_get_tile_owners(const rt_ctx* ctx, int32_t* owner, int32_t n_tiles);
  * the accumulation are left as they were; the stats counters include the probe frames. */
 int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
                   uint64_t* costs);
-/* Longest-first work order (no GL counterpart: the rasteriser schedules fragments itself).  Renders
- * n_frames as a cost probe (as rt_tile_costs, state left unchanged), then reorders this ctx's pixel
+/* Longest-first work order (no GL counterpart: the rasteriser schedules fragments itself).  Traces
+ * the camera pass of n_frames as a cost probe (the camera rays are the same in every frame, so the
+ * costs do not depend on the frames; state left unchanged), then reorders this ctx's pixel
  * list by whole 64-pixel blocks (an 8x8 block stays one wave) in descending cost, so the blocks
  * whose rays cost most are queued first and a pass's tail is the cheap blocks; the costliest 5%
  * become a pixel group of their own in one-frame calls (their long bounce chains reach the
