@@ -1326,6 +1326,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
 #define RT_FINISH_SHADE_MIN 16
 #endif
+#ifndef RT_FINISH_RELOAD
+#define RT_FINISH_RELOAD 1
+#endif
 #ifndef RT_FINISH_HOLD_CONT  // the continuation ray fetched with the shadow ray, held in registers
 #define RT_FINISH_HOLD_CONT 1
 #endif
@@ -1452,7 +1455,20 @@ void wf_finish(const WFParams W) {
       prof_sh++;
 #endif
       const bool sh = st == FS_SHADE;
+#if RT_FINISH_RELOAD
+      // the shade step reads its parameters through an opaque copy of the kernel-argument address,
+      // so their ~30 pointers are loaded here (scalar loads) instead of being held in SGPRs
+      // across the trace loop
+      typedef const __attribute__((address_space(4))) WFParams KArgW;
+      KArgW* Wk = (KArgW*)__builtin_amdgcn_kernarg_segment_ptr();  // W is the only argument
+      asm volatile("" : "+s"(Wk));
+      const WFParams* Wl = (const WFParams*)Wk;
+      const KParams& PL = Wl->K;
+      const Env EL{PL.hdr, PL.cache, PL.light, PL.hdr_w, PL.hdr_h, PL.hdr_res, PL.env_angle, PL.env_intensity};
+      const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, nsamples);
+#else
       const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, nsamples);
+#endif
       if (sh) {
         nsteps++;
         if (o.qShadow || o.qCont) {
