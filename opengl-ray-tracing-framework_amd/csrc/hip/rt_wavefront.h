@@ -1352,7 +1352,9 @@ void wf_finish(const WFParams W) {
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
+#if !RT_FINISH_RELOAD
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
+#endif
   TraceStack TS;
   TS.KL = P.lds_entries;
   TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
