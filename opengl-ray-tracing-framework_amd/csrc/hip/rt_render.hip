@@ -114,7 +114,8 @@ struct rt_ctx {
   unsigned long long* d_tile_cost = nullptr;  // rt_tile_costs: per local tile, during the probe only
   bool tile_cost_on = false;
   bool cost_blocks = false;        // the probe counts per 64-item work block (rt_order_work)
-  float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera)
+  float4* d_cam = nullptr;         // per pixel of this rank: camera direction, u * v (wf_camera), then the
+                                   // per-pixel camera hit points (WFState::org), one of each per set
   int cam_sets = 1;                // camera tables in d_cam (one per pipeline set, n_valid each)
   int n_valid = 0;                 // valid pixels of this rank (work items of the wavefront)
   int frames_cap = 1;              // frames in flight per wavefront
@@ -614,15 +615,22 @@ int occupancy(rt_ctx* c) {
 
 template <bool COUNT, bool WIDE>
 void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
+  // pass 1 reads the 16-B rays pass 0 queued (WFState::org) in an instantiation of its own, so the
+  // later passes' kernel carries none of it
+  const bool p1 = !WP.cam_n && WP.pass == 1 && WP.p1_compact;
   if (small && !COUNT && WIDE) {  // static first shares of mid-size passes
     if (WP.cam_n)
       hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
+    else if (p1)
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true>), grid, dim3(256), c->trace_lds, st, WP);
     else
       hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
     return;
   }
   if (WP.cam_n)
     hipLaunchKernelGGL((rtd::wf_trace<COUNT, WIDE, true>), grid, dim3(256), c->trace_lds, st, WP);
+  else if (p1)
+    hipLaunchKernelGGL((rtd::wf_trace<COUNT, WIDE, false, false, true>), grid, dim3(256), c->trace_lds, st, WP);
   else
     hipLaunchKernelGGL((rtd::wf_trace<COUNT, WIDE, false>), grid, dim3(256), c->trace_lds, st, WP);
 }
@@ -1075,7 +1083,7 @@ static int apply_tiling(rt_ctx* c, int width, int height, const rt_tiling& tl, s
   dfree(c->d_cam);
   const size_t nv = std::max<size_t>(1, xy.size());
   HIPCHK(c, hipMalloc(&c->d_pix, 2 * nv * sizeof(unsigned int)));
-  HIPCHK(c, hipMalloc(&c->d_cam, nv * sizeof(float4)));
+  HIPCHK(c, hipMalloc(&c->d_cam, 2 * nv * sizeof(float4)));
   c->cam_sets = 1;
   if (!xy.empty()) {
     HIPCHK(c, hipMemcpy(c->d_pix, xy.data(), xy.size() * 4, hipMemcpyHostToDevice));
@@ -1236,7 +1244,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     if (c->cam_sets < pipe_sets) {  // one camera table per set (a call may move the camera)
       HIPCHK(c, hipStreamSynchronize(c->stream));
       dfree(c->d_cam);
-      HIPCHK(c, hipMalloc(&c->d_cam, (size_t)std::max(1, c->n_valid) * pipe_sets * sizeof(float4)));
+      HIPCHK(c, hipMalloc(&c->d_cam, 2 * (size_t)std::max(1, c->n_valid) * pipe_sets * sizeof(float4)));
       c->cam_sets = pipe_sets;
       c->wf.cam = c->d_cam;
     }
@@ -1427,6 +1435,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.K.pool_chunk = c->pool_chunk;
         const int set = pipe ? pset : g;  // path-state set, overflow column, stream
         float4* cam = c->wf.cam + (pipe ? (size_t)pset * (size_t)c->n_valid : 0);
+        float4* org = c->wf.cam + (size_t)c->cam_sets * (size_t)std::max(1, c->n_valid) +
+                      (pipe ? (size_t)pset * (size_t)c->n_valid : 0);
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)set * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
         WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds (RT_DEBUG_PASSES)
@@ -1434,6 +1444,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.S.pix_xy = c->wf.pix_xy + w0;
         WP.S.pix_acc = c->wf.pix_acc + w0;
         WP.S.cam = cam + w0;
+        WP.S.org = org + w0;
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
@@ -1480,6 +1491,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         const bool finish = !count && !c->tile_cost_on && !(fp->flags & RT_FLAG_NO_FINISH) &&
                             fin_pass >= 1 && fin_pass <= last_pass &&
                             ((fp->flags & RT_FLAG_FINISH) || slots_g[g] <= c->finish_slots);
+        // pass 0 queues 16-B rays (WFState::org) unless the finisher takes them over at pass 1
+        WP.p1_compact = (finish && fin_pass <= 1) ? 0 : 1;
         for (int pass = 0; pass <= last_pass; pass++) {
           WP.pass = pass;
           if (finish && pass == fin_pass) {

@@ -55,11 +55,27 @@ struct WFState {
   const unsigned int* __restrict__ pix_xy;   // per work item: px | py << 16
   const unsigned int* __restrict__ pix_acc;  // per work item: accumulation index
   float4* __restrict__ cam;                   // per work item: camera direction, u * v (wf_camera)
+  // per work item: the camera hit point of its pixel (pass 0's shade, frame 0 of each pixel).  All
+  // of a pixel's frames share it (R6: the camera ray is the same in every frame), so the rays that
+  // pass 0 queues are stored as 16 B: {d.xyz, s} in ra / sa, origin = org + cam.xyz * s (s = the
+  // medium scattering distance of a continuation, else 0) instead of {o.xyz, d.x} + {d.y, d.z}
+  float4* __restrict__ org;
   int* queue[2];                // ray queue entries: path << 1 | is_shadow
   int* active[2];               // active path ids
   unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
 };
 
+// a ray queued by pass 0 in the 16-B form (see WFState::org): origin and direction
+RTD void p1_ray(const WFState& S, unsigned int n_frames, unsigned int path, const float4 a, float& ox, float& oy,
+                float& oz) {
+  const unsigned int w = path / n_frames;
+  const float4 o = S.org[w];
+  ox = o.x; oy = o.y; oz = o.z;
+  if (a.w != 0.0f) {  // a scattered continuation: hP + hV * scatterDist, as pass 0's shade computed it
+    const float4 c = S.cam[w];
+    ox = o.x + c.x * a.w; oy = o.y + c.y * a.w; oz = o.z + c.z * a.w;
+  }
+}
 RTD void put_ray(float4* a, float2* b, unsigned int p, float ox, float oy, float oz, float dx, float dy, float dz) {
   a[p] = make_float4(ox, oy, oz, dx);
   b[p] = make_float2(dy, dz);
@@ -74,6 +90,7 @@ struct WFParams {
   // paths of slots [0, cam_n) in slot order (entry i = slot i), generated where they are used
   // (wf_trace refill, wf_shade) instead of being written by a generation kernel and read back
   unsigned int cam_n;
+  int p1_compact;  // pass 0 queues 16-B rays from the per-pixel origin (off when the finisher starts at pass 1)
   // one frame per path-state set and nothing in flight before it (unpipelined calls of one frame
   // per group): a finishing path blends into the accumulation itself (wf_blend's operations,
   // RT:1552) instead of writing fin for a wf_blend launch after the last pass
@@ -653,7 +670,7 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
 // passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
 // a separate instantiation: the code alone cost the bulk's kernels 0.4%)
-template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false>
+template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false>  // P1: pass 1's 16-B rays
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -760,9 +777,14 @@ void wf_trace(const WFParams W) {
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
             const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
-            const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
-            L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
-            L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
+            if (P1) {  // 16-B rays from pass 0
+              p1_ray(S, (unsigned)W.n_frames, (unsigned)path, oa, L.ox, L.oy, L.oz);
+              L.dx = oa.x; L.dy = oa.y; L.dz = oa.z;
+            } else {
+              const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
+              L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
+              L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
+            }
           }
           tl_start<WIDE>(P, L);
           busy = true;
@@ -939,10 +961,22 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       }
     }
     const int2 rc0 = S.res[2 * path];
-    const float4 ra0 = camPass ? make_float4(P.pos[0], P.pos[1], P.pos[2], cam_d.x) : S.ra[path];
-    const float2 rb0 = camPass ? make_float2(cam_d.y, cam_d.z) : S.rb[path];
-    const float4 oo0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
-    const float4 dd0 = make_float4(ra0.w, rb0.x, rb0.y, 0.0f);
+    float4 oo0, dd0;
+    if (camPass) {
+      oo0 = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
+      dd0 = make_float4(cam_d.x, cam_d.y, cam_d.z, 0.0f);
+    } else if (W.p1_compact && W.pass == 1) {  // (uniform) the continuation in pass 0's 16-B form
+      const float4 ra0 = S.ra[path];
+      float ox, oy, oz;
+      p1_ray(S, (unsigned)W.n_frames, (unsigned)path, ra0, ox, oy, oz);
+      oo0 = make_float4(ox, oy, oz, 0.0f);
+      dd0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
+    } else {
+      const float4 ra0 = S.ra[path];
+      const float2 rb0 = S.rb[path];
+      oo0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
+      dd0 = make_float4(ra0.w, rb0.x, rb0.y, 0.0f);
+    }
     wseed = a5.x; bounce = a5.y; flags = a5.z; frame = a5.w;
     if (!(flags & PF_CAMERA)) {
       hist = xyz(a0); evp = a0.w;
@@ -996,6 +1030,9 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
           bounce++;
         }
         hP = Pp;
+        // pass 0: frame 0 of each pixel records the camera hit point, the origin of every frame's
+        // next rays (WFState::org)
+        if (camPass && W.p1_compact && frame == 0u) S.org[(unsigned)path / (unsigned)W.n_frames] = make_float4(Pp.x, Pp.y, Pp.z, 0.0f);
         hN = inside ? -Ns : Ns;
         hV = rd;
         hDist = t - 0.00001f;
@@ -1044,6 +1081,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   f3 cnee = splat(0.0f), cmed = splat(0.0f);
   uint32_t nflags = 0;
   f3 contO = splat(0.0f), contD = splat(0.0f), shO = splat(0.0f), shD = splat(0.0f);
+  float contS = 0.0f;  // the continuation's scattering distance (its origin = hit point + hV * contS)
   float bNdotL = 0.0f;  // BRDF mode: N.L of the sampled direction (RT:1336)
   if (doBounce && !BSDF) {  // shadingImportanceSampling_BRDF, one iteration (RT:1296-1365)
     const Mat m = load_mat(P.mats, mat);
@@ -1145,6 +1183,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
         const float scatterDist = min_(-log_(xi_3) / m.mdensity, hDist);
         medS = scatterDist < hDist;
         if (medS) {
+          contS = scatterDist;
           transmittance *= exp_(-1.0f * scatterDist);
           hist = hist * (m.mcolor * transmittance);
           hP = hP + hV * scatterDist;
@@ -1197,11 +1236,12 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
     if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
     S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
-    if (qCont) {
-      put_ray(S.ra, S.rb, path, contO.x, contO.y, contO.z, contD.x, contD.y, contD.z);
-    }
-    if (qShadow) {
-      put_ray(S.sa, S.sb, path, shO.x, shO.y, shO.z, shD.x, shD.y, shD.z);
+    if (camPass && W.p1_compact) {  // (uniform) 16-B rays from the pixel's camera hit point
+      if (qCont) S.ra[path] = make_float4(contD.x, contD.y, contD.z, contS);
+      if (qShadow) S.sa[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
+    } else {
+      if (qCont) put_ray(S.ra, S.rb, path, contO.x, contO.y, contO.z, contD.x, contD.y, contD.z);
+      if (qShadow) put_ray(S.sa, S.sb, path, shO.x, shO.y, shO.z, shD.x, shD.y, shD.z);
     }
   }
   return ShadeOut{qShadow, qCont};

@@ -27,9 +27,12 @@ for r in rows:
 
 
 def short(n):
-    n = n.replace("rtd::", "").split("(")[0]
-    return n.replace("wf_trace<false, true, false, true>", "trace_s").replace("wf_trace<false, true, true, true>", "trace_cam_s").replace("wf_trace<false, true, false, false>", "trace").replace("wf_trace<false, true, true, false>", "trace_cam") \
-            .replace("wf_shade<true, true>", "shade_fb").replace("wf_shade<true, false>", "shade") \
+    n = n.replace("rtd::", "").replace("void ", "").split("(")[0].strip()
+    if n.startswith("wf_trace<"):  # <COUNT, WIDE, CAM, STATIC, P1>
+        f = [x.strip() == "true" for x in n[len("wf_trace<"):-1].split(",")]
+        f += [False] * (5 - len(f))
+        return ("trace_cnt" if f[0] else "trace") + ("_cam" if f[2] else "") + ("_p1" if f[4] else "") + ("_s" if f[3] else "")
+    return n.replace("wf_shade<true, true>", "shade_fb").replace("wf_shade<true, false>", "shade") \
             .replace("wf_shade<false, true>", "shade_brdf_fb").replace("wf_shade<false, false>", "shade_brdf")
 
 
