@@ -54,8 +54,10 @@ B_INT, B_LEAF, B_TRI, B_UPD, B_ENV, B_CACHE, B_PIXEL = 64, 16, 36, 132, 12, 12, 
 # secondary ray reads its 4-B queue entry and its 24-B origin/direction (WFState ra/rb or sa/sb:
 # {o.xyz, d.x} float4 + {d.y, d.z} float2) and writes its 8-B result; a camera ray is rebuilt from
 # the per-pixel camera table (16 B per pixel, shared by the pixel's frames) and writes its 8-B
-# result (tests/test_bench_cpu.py pins these to the WFState layout)
-B_RAY_SECONDARY, B_RAY_CAMERA = 4 + 24 + 8, 8
+# result; pass 1's rays (rt_stats.p1_rays) are 16-B records {d, scattering distance} whose origin
+# is the pixel's camera hit point (WFState org, 16 B per pixel, shared by the pixel's frames)
+# (tests/test_bench_cpu.py pins these to the WFState layout)
+B_RAY_SECONDARY, B_RAY_PASS1, B_RAY_CAMERA = 4 + 24 + 8, 4 + 16 + 8, 8
 # wf_trace's own traversal bytes per visit (served from L2 / MALL): a 128-B 4-wide node, a
 # 48-B triangle record
 B_QNODE, B_TRI_REC = 128, 48
@@ -261,7 +263,8 @@ def roofline(st, vis, cnt, prof, trace_ms):
     launches = max(1, st["trace_launches"])
     rays_l = st["rays"] / launches
     cam_l = st["samples"] / launches                      # one camera ray per sample
-    alg = (B_RAY_SECONDARY * (rays_l - cam_l) + B_RAY_CAMERA * cam_l)
+    p1_l = st.get("p1_rays", 0) / launches                # pass 1: 16-B ray records
+    alg = (B_RAY_SECONDARY * (rays_l - cam_l - p1_l) + B_RAY_PASS1 * p1_l + B_RAY_CAMERA * cam_l)
     sec = trace_ms * 1e-3
     out = {"bound": "hbm", "limiter": None, "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
@@ -269,7 +272,8 @@ def roofline(st, vis, cnt, prof, trace_ms):
            "avg_launch_ms_note": "HIP events on the launch stream during the timed steps (the other frame "
                                  "group's wf_shade co-runs)",
            "rays_per_launch": round(rays_l), "algorithmic_bytes_per_launch": round(alg),
-           "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "camera": B_RAY_CAMERA}}
+           "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "pass1": B_RAY_PASS1, "camera": B_RAY_CAMERA},
+           "pass1_rays_per_launch": round(p1_l)}
     util = {"hbm": out["frac"]}
     pt = (prof or {}).get("kernels", {}).get("wf_trace")
     if pt:

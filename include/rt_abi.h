@@ -113,6 +113,7 @@ typedef struct rt_stats {
   uint64_t trace_iters;     /* RT_FLAG_COUNT_VISITS: traversal loop iterations, all waves */
   uint64_t trace_iters_max; /* RT_FLAG_COUNT_VISITS: max loop iterations of one wave       */
   uint64_t path_steps;      /* wavefront path: shade steps (one per path per bounce pass)  */
+  uint64_t p1_rays;         /* wavefront path: rays traced from pass 0's 16-B ray records  */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

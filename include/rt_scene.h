@@ -121,6 +121,12 @@ int rts_cpu_rand_origins(unsigned int seed, int n, float* out);
  * restated; identical to the libc's on glibc systems). */
 int rts_glibc_rand(unsigned int seed, int n, int* out);
 
+/* The HIP path's traversal records and edge-filter margin (csrc/common/tri_filter.h; rt_set_scene
+ * builds them the same way): tri = 3 float[4] per triangle {p1, N.x} {p2, N.y} {p3, N.z}, out = 3
+ * float[4] per triangle {p1, N.x} {R2, N.y} {R3, N.z}; k = {k1, k0}; flagged = triangles left to the
+ * reference's edge functions alone.  For tests: it replaces no reference interface. */
+int rts_tri_filter(const float* tri, int n_triangles, float* out, double* k, int32_t* flagged);
+
 /* 8-bit RGB PNG (stbi_write_png in SaveFrame, src/core/Utility.h:19-30): width*height*3 bytes,
  * row 0 = top (rt_tonemap's output order).  Stored (uncompressed) deflate, no zlib needed. */
 int rts_write_png(const char* path, int width, int height, const uint8_t* rgb);

@@ -52,6 +52,8 @@ struct KParams {
   int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]
   unsigned int ovf_lanes;
   const float4* __restrict__ tri;   // 3 per triangle: {p1, Ng.x} {p2, Ng.y} {p3, Ng.z}
+  const float4* __restrict__ trx;   // traversal record, 3 per triangle: {p1, Ng.x} {R2, Ng.y} {R3, Ng.z}
+  float tri_k1, tri_k0;             // its edge-filter margin (csrc/common/tri_filter.h)
   const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, leaf rank bits} {n3, 0}
   const float4* __restrict__ mats;  // 8 per material
   const float4* __restrict__ hdr;

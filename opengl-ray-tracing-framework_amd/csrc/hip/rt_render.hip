@@ -19,6 +19,7 @@
 #include "rt_abi.h"
 #include "rt_kernels.h"
 #include "rt_wavefront.h"
+#include "tri_filter.h"
 
 using rtd::GNode;
 using rtd::KParams;
@@ -35,6 +36,9 @@ struct rt_ctx {
   int qroot = 0, qstack_entries = 2;
   bool wide = false;                          // 4-wide traversal available for this scene
   float4* d_tri = nullptr;
+  float4* d_trx = nullptr;  // traversal records (tri_filter.h)
+  double tri_k1 = 0.0, tri_k0 = 0.0;  // their edge-filter margin
+  int tri_flagged = 0;
   float4* d_trin = nullptr;
   float4* d_mats = nullptr;
   int n_tri = 0, n_mats = 0, root = 0, has_scene = 0, stack_entries = 2;
@@ -769,7 +773,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
-  dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trin); dfree(c->d_mats);
+  dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trx); dfree(c->d_trin); dfree(c->d_mats);
   for (auto& t : c->light) {
     dfree(t.d);
     if (t.last_use) (void)hipEventDestroy(t.last_use);
@@ -915,6 +919,12 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, (void**)&c->d_qnodes, qn.data(), qn.size() * sizeof(rtd::QNode)))) return rc;
   if ((rc = upload(c, (void**)&c->d_nodes, gn.data(), gn.size() * sizeof(GNode)))) return rc;
   if ((rc = upload(c, (void**)&c->d_tri, tri.data(), tri.size() * sizeof(float4)))) return rc;
+  {  // traversal records: {p1, Ng.x} {R2, Ng.y} {R3, Ng.z} and the edge filter's margin
+    std::vector<float4> trx(std::max<size_t>(3, tri.size()));
+    const trif::Consts k = trif::build(reinterpret_cast<const float*>(tri.data()), nt, reinterpret_cast<float*>(trx.data()));
+    if ((rc = upload(c, (void**)&c->d_trx, trx.data(), trx.size() * sizeof(float4)))) return rc;
+    c->tri_k1 = k.k1; c->tri_k0 = k.k0; c->tri_flagged = k.flagged;
+  }
   if ((rc = upload(c, (void**)&c->d_trin, trin.data(), trin.size() * sizeof(float4)))) return rc;
   if ((rc = upload(c, (void**)&c->d_mats, mt.data(), mt.size() * sizeof(float)))) return rc;
   c->n_tri = nt;
@@ -1363,6 +1373,14 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       P.cull_eps = (eps * sc < 1e30) ? (float)(eps * sc) : INFINITY;
     }
     P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
+    {  // edge-filter margin, rounded up (x (1 + 2^-20)); RT_TRI_MARGIN_SCALE (tests only): 0 makes
+       // the filter decide every point, the negative control of tests/test_gpu_tri_filter.py
+      const char* ms = knob("RT_TRI_MARGIN_SCALE");
+      const double sc = ms ? atof(ms) : 1.0;
+      P.trx = c->d_trx;
+      P.tri_k1 = (float)(c->tri_k1 * sc * (1.0 + 0x1p-20));
+      P.tri_k0 = (float)(c->tri_k0 * sc * (1.0 + 0x1p-20));
+    }
     P.hdr = c->d_hdr; P.cache = c->d_cache; P.light = LT->d;
     P.hdr_w = c->hdr_w; P.hdr_h = c->hdr_h; P.hdr_res = c->hdr_res;
     P.accum = c->d_accum; P.counter = c->d_counter; P.stats = c->d_stats;
@@ -1730,9 +1748,10 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->trace_ms = c->trace_ms;
   st->trace_iters = h[5];
   st->trace_iters_max = h[6];
-  unsigned long long ps = 0;
-  HIPCHK(c, hipMemcpy(&ps, c->d_stats + 16, sizeof(ps), hipMemcpyDeviceToHost));
-  st->path_steps = ps;
+  unsigned long long ps[2] = {0, 0};
+  HIPCHK(c, hipMemcpy(ps, c->d_stats + 16, sizeof(ps), hipMemcpyDeviceToHost));
+  st->path_steps = ps[0];
+  st->p1_rays = ps[1];
   return RT_OK;
 }
 

@@ -329,10 +329,26 @@ RTD bool tie_wins(const KParams& P, const TraceLane& L, int a, int b) {
   return a < b;
 }
 
-// one triangle (RT:241-299, R1); true when it becomes the closest hit
+// The reference's three edge functions (RT:273-281) on the computed hit point: only for the
+// points the barycentric filter below cannot decide (p2, p3 from the shading record P.tri).
+RTD bool tl_edges_exact(const KParams& P, int i, const f3 p1, const f3 ng, const f3 Pp) {
+  const uint32_t off = (uint32_t)i * 48u;
+  const f3 p2 = xyz(ld<float4>(P.tri, off + 16u)), p3 = xyz(ld<float4>(P.tri, off + 32u));
+  const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
+  const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
+  const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
+  return (e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0);
+}
+
+// one triangle (RT:241-299, R1); true when it becomes the closest hit.  {A, B, Cc} = the traversal
+// record {p1, Ng.x} {R2, Ng.y} {R3, Ng.z} (csrc/common/tri_filter.h): the plane test and t are the
+// reference's operations; "inside" is decided by the barycentric rows b2 = R2.(P - p1),
+// b3 = R3.(P - p1), b1 = 1 - b2 - b3 whenever min(b) lies outside the error margin
+// m = k1 * max|P - p1| * (max|R2| + max|R3|) + k0 that bounds both b's error and the fp32 error of
+// the reference's edge functions (tri_filter.h derives it), else by those edge functions.
 template <bool WIDE>
 RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
-  const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+  const f3 p1 = xyz(A);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d());
   if (fabs_(dn) < 0.00001f) return false;                           // RT:262
@@ -347,10 +363,19 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   const float dist = t - 0.00001f;
   if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
   const f3 Pp = L.o() + L.d() * t;
-  const float e1 = dot(cross(p2 - p1, Pp - p1), ng);
-  const float e2 = dot(cross(p3 - p2, Pp - p2), ng);
-  const float e3 = dot(cross(p1 - p3, Pp - p3), ng);
-  if (!((e1 > 0 && e2 > 0 && e3 > 0) || (e1 < 0 && e2 < 0 && e3 < 0))) return false;
+  const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
+  const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
+  const float b3 = __builtin_fmaf(Cc.x, qx, __builtin_fmaf(Cc.y, qy, Cc.z * qz));
+  const float b1 = (1.0f - b2) - b3;
+  const float mn = fminf(b1, fminf(b2, b3));
+  const float dq = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
+  const float lr = fmaxf(fabsf(B.x), fmaxf(fabsf(B.y), fabsf(B.z))) + fmaxf(fabsf(Cc.x), fmaxf(fabsf(Cc.y), fabsf(Cc.z)));
+  const float m = (dq * lr) * P.tri_k1 + P.tri_k0;
+  if (fabsf(mn) > m && m < 0.25f) {
+    if (!(mn > 0.0f)) return false;
+  } else if (!tl_edges_exact(P, i, p1, ng, Pp)) {
+    return false;
+  }
   if (WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
   L.best = dist;
   L.besttri = i;
@@ -360,7 +385,7 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
 template <bool WIDE>
 RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   const uint32_t off = (uint32_t)i * 48u;
-  const float4 A = ld<float4>(P.tri, off), B = ld<float4>(P.tri, off + 16u), Cc = ld<float4>(P.tri, off + 32u);
+  const float4 A = ld<float4>(P.trx, off), B = ld<float4>(P.trx, off + 16u), Cc = ld<float4>(P.trx, off + 32u);
   return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc);
 }
 
@@ -599,15 +624,15 @@ RTD DualLoad tl_dual_load(const KParams& P, const TraceLane& L, bool active) {
   d.A = d.B = d.Cc = d.A2 = d.B2 = d.C2 = make_float4(0, 0, 0, 0);
   if (d.doTri) {
     const uint32_t off = (uint32_t)L.tri_i * 48u;
-    d.A = ld<float4>(P.tri, off);
-    d.B = ld<float4>(P.tri, off + 16u);
-    d.Cc = ld<float4>(P.tri, off + 32u);
+    d.A = ld<float4>(P.trx, off);
+    d.B = ld<float4>(P.trx, off + 16u);
+    d.Cc = ld<float4>(P.trx, off + 32u);
   }
   if (d.doTri2) {
     const uint32_t off = (uint32_t)L.tri_i * 48u + 48u;
-    d.A2 = ld<float4>(P.tri, off);
-    d.B2 = ld<float4>(P.tri, off + 16u);
-    d.C2 = ld<float4>(P.tri, off + 32u);
+    d.A2 = ld<float4>(P.trx, off);
+    d.B2 = ld<float4>(P.trx, off + 16u);
+    d.C2 = ld<float4>(P.trx, off + 32u);
   }
   if (d.doNode) d.q = tl_qnode_load(P, L);
   return d;
@@ -1267,7 +1292,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   }
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) nrays = nq_in;  // rays traced by the pass before us
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    nrays = nq_in;  // rays traced by the pass before us
+    if (W.pass == 1 && W.p1_compact && nq_in) atomicAdd(&P.stats[17], (unsigned long long)nq_in);  // rt_stats.p1_rays
+  }
   for (unsigned int base = blockIdx.x * (256u * SH_SUB); base < na; base += gridDim.x * (256u * SH_SUB)) {
   // ---- group the block's paths by what they will execute (block-local counting sort in LDS):
   // divergence between a continuation that missed (env lookup) and one that hit (a full BSDF

@@ -7,6 +7,7 @@
 // reproduces the reference's BVH node arrays bit for bit.  Compiled with
 // -ffp-contract=off (no FMA contraction, as the reference's x86-64 SSE build).
 #include "rt_scene.h"
+#include "tri_filter.h"
 
 #include <math.h>
 #include <stdio.h>
@@ -1291,3 +1292,12 @@ int rts_cpu_rand_origins(unsigned int seed, int n, float* out) {
 }
 
 }  // extern "C"
+
+int rts_tri_filter(const float* tri, int n_triangles, float* out, double* k, int32_t* flagged) {
+  if (n_triangles < 0 || (n_triangles && (!tri || !out)) || !k) return RTS_ERR_ARG;
+  const trif::Consts c = trif::build(tri, n_triangles, out);
+  k[0] = c.k1;
+  k[1] = c.k0;
+  if (flagged) *flagged = c.flagged;
+  return 0;
+}

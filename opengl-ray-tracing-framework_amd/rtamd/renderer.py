@@ -80,7 +80,8 @@ class RtStats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("samples", C.c_uint64), ("internal_pops", C.c_uint64),
                 ("leaf_pops", C.c_uint64), ("tri_tests", C.c_uint64), ("launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("trace_launches", C.c_uint64), ("trace_ms", C.c_double),
-                ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64), ("path_steps", C.c_uint64)]
+                ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64), ("path_steps", C.c_uint64),
+                ("p1_rays", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -113,6 +113,7 @@ def lib() -> C.CDLL:
         L.rts_cpu_rand_origins.argtypes = [C.c_uint, C.c_int, _f32p]
         L.rts_glibc_rand.argtypes = [C.c_uint, C.c_int, C.POINTER(C.c_int)]
         L.rts_write_png.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]
+        L.rts_tri_filter.argtypes = [_f32p, C.c_int, _f32p, C.POINTER(C.c_double), _i32p]
         _lib = L
     return _lib
 
@@ -313,6 +314,18 @@ def glibc_rand(seed: int, n: int) -> np.ndarray:
     out = np.zeros(n, np.int32)
     _check(lib().rts_glibc_rand(seed, n, out.ctypes.data_as(C.POINTER(C.c_int))), "rts_glibc_rand")
     return out
+
+
+def tri_filter(tri: np.ndarray):
+    """Traversal records {p1, N.x} {R2, N.y} {R3, N.z} and the edge-filter margin (k1, k0) of the
+    HIP path (csrc/common/tri_filter.h) for tri = (n, 3, 4) float32 {p1, N.x} {p2, N.y} {p3, N.z}."""
+    tri = np.ascontiguousarray(tri, np.float32)
+    n = tri.shape[0]
+    out = np.zeros_like(tri)
+    k = (C.c_double * 2)()
+    fl = np.zeros(1, np.int32)
+    _check(lib().rts_tri_filter(_fp(tri), n, _fp(out), k, _ip(fl)), "rts_tri_filter")
+    return out, float(k[0]), float(k[1]), int(fl[0])
 
 
 def write_png(path: str, rgb: np.ndarray) -> None:

@@ -93,6 +93,7 @@ def test_trace_ray_bytes_follow_the_path_state_layout():
     assert "float4* __restrict__ sa;" in src and "float2* __restrict__ sb;" in src
     assert "int2* __restrict__ res;" in src
     assert bench.B_RAY_SECONDARY == 4 + (16 + 8) + 8
+    assert bench.B_RAY_PASS1 == 4 + 16 + 8  # WFState ra/sa float4 only (p1_ray): origin from org
     assert bench.B_RAY_CAMERA == 8
 
 
@@ -109,6 +110,8 @@ def test_roofline_names_its_limiter_at_the_spec_clock():
         "wf_shade": {"avg_launch_ms": 13.0, "avg_launch_ms_standalone": 6.0, "hbm_bytes_per_launch": 3.0e10}}}
     r = bench.roofline(st, vis, None, prof, 16.0)
     assert r["bound"] == "hbm" and r["kernel"] == "wf_trace"
+    r1 = bench.roofline(dict(st, p1_rays=500_000_000), vis, None, prof, 16.0)
+    assert r["algorithmic_bytes_per_launch"] - r1["algorithmic_bytes_per_launch"] == 50_000_000 * 8
     assert r["valu"]["spec_clock_ghz"] == 2.4
     want = 6.6e9 * 2 / (1024 * 2.4e9 * 12e-3)
     assert abs(r["valu"]["issue_frac_at_spec_clock"] - want) < 1e-4

@@ -33,6 +33,21 @@ def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     assert frac == 0.0, f"{name}: {frac:.4%} of pixels differ from the oracle"
 
 
+def test_pass1_ray_count(gpu_renderer, env_maps):
+    """rt_stats.p1_rays (bench.py prices these rays at their 16-B records): without the finisher,
+    pass 1 traces the shadow rays and continuations pass 0 queued, so camera + pass-1 rays never
+    exceed the total and, with the dragon in view, pass 1 is not empty."""
+    from rtamd.renderer import RT_FLAG_NO_FINISH
+    sd = cf.config_scene("C3")
+    W, H = 96, 54
+    fp = cf.frame_params(W, H, flags=RT_FLAG_NO_FINISH)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    img, st = gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    assert bit_mismatch(img, ref)[0] == 0.0 and st["rays"] == cnt["rays"]
+    assert 0 < st["p1_rays"] and st["samples"] + st["p1_rays"] <= st["rays"], st
+
+
 def test_no_cull_matches_too(gpu_renderer, env_maps):
     sd = cf.config_scene("C3")
     W, H = 64, 36

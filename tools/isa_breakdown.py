@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("asm")
 ap.add_argument("kernel")
 ap.add_argument("--json")
+ap.add_argument("--dump", help="print the instructions of this source function")
 a = ap.parse_args()
 src_dir = Path(__file__).resolve().parent.parent / "opengl-ray-tracing-framework_amd" / "csrc"
 
@@ -80,6 +81,8 @@ for ln in lines[start + 1:]:
             "vmem" if op.startswith(("global_", "buffer_", "flat_", "scratch_")) else "lds" if op.startswith("ds_") else "other")
     fn = region_maps.get(loc[0], {}).get(loc[1]) or f"{loc[0]}"
     cnt[fn][kind] += 1
+    if a.dump and fn == a.dump:
+        print(f"{loc[1]:5d}  {t}")
 rows = sorted(cnt.items(), key=lambda kv: -(kv[1]["valu"] + kv[1]["salu"]))
 print(f"{kname}: static instructions by source function")
 print(f"{'function':28s} {'VALU':>6s} {'SALU':>6s} {'VMEM':>5s} {'LDS':>4s}")
