@@ -348,20 +348,16 @@ RTD bool tl_edges_exact(const KParams& P, int i, const f3 p1, const f3 ng, const
 // the reference's edge functions (tri_filter.h derives it), else by those edge functions.
 template <bool WIDE>
 RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
+  // straight-line form: every condition of RT:262-281 folded into one predicate (a 64-lane wave
+  // runs the whole test for some lane anyway; early returns, and round 2's rcp-based pre-reject
+  // ahead of the division, only cost exec-mask juggling: +1.3% C3, profiles/r03_ab_bulk_tri_flat_C3.log)
   const f3 p1 = xyz(A);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   const float dn = dot(ng, L.d());
-  if (fabs_(dn) < 0.00001f) return false;                           // RT:262
   const float num = dot(ng, p1) - dot(L.o(), ng);
-  // Conservative early reject before the correctly rounded division: num * rcp(dn) is within
-  // ~2^-21 of num / dn (|dn| >= 1e-5, no denormals), so outside these margins the exact t
-  // fails RT:268 or the closest-hit test for certain.  NaN never rejects.
-  const float qa = num * __builtin_amdgcn_rcpf(dn);
-  if (qa < 0.0005f * (1.0f - 0x1p-16f)) return false;
-  if (qa > (L.best + 0.00001f) * (1.0f + 0x1p-16f)) return false;
   const float t = num / dot(L.d(), ng);                                // RT:265
   const float dist = t - 0.00001f;
-  if (!(t >= 0.0005f && (WIDE ? dist <= L.best : dist < L.best))) return false;  // RT:268, RT:328/356
+  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (WIDE ? dist <= L.best : dist < L.best);  // RT:262, 268, 328/356
   const f3 Pp = L.o() + L.d() * t;
   const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
   const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
@@ -371,16 +367,16 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   const float dq = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
   const float lr = fmaxf(fabsf(B.x), fmaxf(fabsf(B.y), fabsf(B.z))) + fmaxf(fabsf(Cc.x), fmaxf(fabsf(Cc.y), fabsf(Cc.z)));
   const float m = (dq * lr) * P.tri_k1 + P.tri_k0;
-  if (fabsf(mn) > m && m < 0.25f) {
-    if (!(mn > 0.0f)) return false;
-  } else if (!tl_edges_exact(P, i, p1, ng, Pp)) {
-    return false;
+  bool inside = mn > 0.0f;
+  if (ok & !((fabsf(mn) > m) & (m < 0.25f))) inside = tl_edges_exact(P, i, p1, ng, Pp);
+  ok &= inside;
+  if (WIDE && ok && dist == L.best) ok = L.besttri >= 0 && tie_wins(P, L, i, L.besttri);
+  if (ok) {
+    L.best = dist;
+    L.besttri = i;
+    L.bestt = t;
   }
-  if (WIDE && dist == L.best && (L.besttri < 0 || !tie_wins(P, L, i, L.besttri))) return false;
-  L.best = dist;
-  L.besttri = i;
-  L.bestt = t;
-  return true;
+  return ok;
 }
 template <bool WIDE>
 RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
@@ -616,11 +612,12 @@ struct DualLoad {
   QLoad q;
   bool doTri, doTri2, doNode;
 };
+template <bool PAIR = RT_FINISH_TRI_PAIR>
 RTD DualLoad tl_dual_load(const KParams& P, const TraceLane& L, bool active) {
   DualLoad d;
   d.doTri = active && L.tri_i < L.tri_end;
   d.doNode = active && L.haveCur && !ref_is_leaf(L.cur);
-  d.doTri2 = RT_FINISH_TRI_PAIR && d.doTri && L.tri_i + 1 < L.tri_end;
+  d.doTri2 = PAIR && d.doTri && L.tri_i + 1 < L.tri_end;
   d.A = d.B = d.Cc = d.A2 = d.B2 = d.C2 = make_float4(0, 0, 0, 0);
   if (d.doTri) {
     const uint32_t off = (uint32_t)L.tri_i * 48u;
@@ -821,6 +818,11 @@ void wf_trace(const WFParams W) {
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
     if (COUNT) { v_itN++; v_itT++; }
+#ifdef RT_TRACE_PREFETCH  // measurement variant: both fetches of a dual step first (tl_dual_load)
+    if (!COUNT && WIDE && busy) {
+      finished = tl_dual_calc(P, L, TS, cull, tl_dual_load<false>(P, L, true));
+    } else
+#endif
     if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
