@@ -277,6 +277,7 @@ struct TraceLane {
   RTD f3 d() const { return mk3(dx, dy, dz); }
   RTD f3 inv() const { return mk3(ix, iy, iz); }
   float best, bestt;
+  RTD float limit(float eps) const { return cull_limit(best, eps, ix, iy, iz); }
   int besttri, sp, cur, tri_i, tri_end;
   int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
   bool haveCur, anyhit, finite;
@@ -393,7 +394,7 @@ RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
 
 // pop the next surviving subtree (RT:348); false when the stack is exhausted
 RTD bool tl_pop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
-  const float lim = cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz);
+  const float lim = L.limit(P.cull_eps);
   while (L.sp > 0) {
     --L.sp;
     const int2 ent = L.sp < S.KL ? S.lds[L.sp * TL_LANES] : unpack_ent(S.ovf[(size_t)(L.sp - S.KL) * S.ovs]);
@@ -426,7 +427,7 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
   } else if (d2 > 0) {
     nearRef = ref.y; nearE = e2; descend = true;
   }
-  if (descend && cull && nearE > cull_limit(L.best, P.cull_eps, L.ix, L.iy, L.iz)) descend = false;
+  if (descend && cull && nearE > L.limit(P.cull_eps)) descend = false;
   L.cur = nearRef;
   L.haveCur = descend || tl_pop(P, L, S, cull);
 }
@@ -440,7 +441,7 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
 // exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
 RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4 rf, const float4 p0, const float4 p1,
                        const float4 p2, const float4 p3, const float4 p4, const float4 p5, float (&k)[4], int (&r)[4]) {
-  const float lim = cull ? cull_limit(L.best, cull_eps, L.ix, L.iy, L.iz) : __int_as_float(0x7f800000);
+  const float lim = cull ? L.limit(cull_eps) : __int_as_float(0x7f800000);
   auto keep = [&](int c, float t0, float t1, int ref) {
     const bool ok = t1 >= t0 && t1 > 0.0f && (!cull || !(t0 > lim));
     k[c] = ok ? t0 : __int_as_float(0x7f800000);
