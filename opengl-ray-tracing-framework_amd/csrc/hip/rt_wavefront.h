@@ -819,11 +819,6 @@ void wf_trace(const WFParams W) {
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
     if (COUNT) { v_itN++; v_itT++; }
-#ifdef RT_TRACE_PREFETCH  // measurement variant: both fetches of a dual step first (tl_dual_load)
-    if (!COUNT && WIDE && busy) {
-      finished = tl_dual_calc(P, L, TS, cull, tl_dual_load<false>(P, L, true));
-    } else
-#endif
     if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
