@@ -28,6 +28,7 @@ ap.add_argument("--reps", type=int, default=1)
 ap.add_argument("--worlds", default="1,2,4,8")
 ap.add_argument("--tile", type=int, default=32)
 ap.add_argument("--out", default=None)
+ap.add_argument("--probe-frames", type=int, default=1, help="frames of the tile-cost probe (bench.py: 1)")
 ap.add_argument("--pipeline", type=int, default=1, help="rt_set_pipeline depth (calls in flight together)")
 ap.add_argument("--calls", type=int, default=1, help="render calls per step (the step's frames split evenly)")
 ap.add_argument("--assign", default="both", choices=["modulo", "balanced", "both"],
@@ -38,7 +39,7 @@ sd = cf.config_scene(a.config)
 env = cf.load_env()
 W, H = cfg.width, cfg.height
 fp = cf.frame_params(W, H)
-ro = cf.rand_origins(a.frames + 1)
+ro = cf.rand_origins(a.frames + a.probe_frames)
 r = Renderer(0)
 r.set_pipeline(a.pipeline)
 r.set_scene_soa(sd.soa, sd.nodes)
@@ -46,7 +47,7 @@ r.set_env(*env)
 lines = []
 # full-frame tile costs (what bench.py's ranks assemble from their shares with an all_reduce)
 r.resize(W, H, tile=a.tile)
-costs = r.tile_costs(fp, ro[-1:])
+costs = r.tile_costs(fp, ro[-a.probe_frames:])
 t1 = None
 modes = ["modulo", "balanced"] if a.assign == "both" else [a.assign]
 for world, mode in [(int(x), m) for x in a.worlds.split(",") for m in modes]:
