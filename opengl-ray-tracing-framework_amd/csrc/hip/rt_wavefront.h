@@ -477,7 +477,10 @@ RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4
     generic(3, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, rf.w);
   }
 }
-RTD void tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, float (&k)[4], int (&r)[4]) {
+// POP: pop the next subtree when no child was entered; without it the caller pops (returns true
+// when it must)
+template <bool POP = true>
+RTD bool tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, float (&k)[4], int (&r)[4]) {
   const int n = (r[0] != Q_EMPTY) + (r[1] != Q_EMPTY) + (r[2] != Q_EMPTY) + (r[3] != Q_EMPTY);
   // valid children sort ahead of empty slots unless a valid entry key is +inf (degenerate)
   const bool ordered = !((r[0] != Q_EMPTY && !(k[0] < INFINITY)) || (r[1] != Q_EMPTY && !(k[1] < INFINITY)) ||
@@ -510,9 +513,12 @@ RTD void tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool
     if (r[1] != Q_EMPTY) tl_push(L, S, e1);
   }
   L.cur = r[0];
+  if (!POP) return r[0] == Q_EMPTY;
   L.haveCur = r[0] != Q_EMPTY || tl_pop(P, L, S, cull);
+  return false;
 }
-RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+template <bool POP = true>
+RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
   const uint32_t off = (uint32_t)L.cur << 7;
   const int4 rf = ld<int4>(P.qnodes, off + 96u);
   float k[4];
@@ -529,7 +535,7 @@ RTD void tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
                  hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
     tl_qnode_keys(L, cull, P.cull_eps, rf, lx, ly, lz, hx, hy, hz, k, r);
   }
-  tl_qnode_push(P, L, S, cull, k, r);
+  return tl_qnode_push<POP>(P, L, S, cull, k, r);
 }
 // the node fetch alone (the finisher issues it before its triangle test): rf + six planes, near /
 // far for a finite 1/d, lo / hi otherwise (tl_start's offsets cover both)
@@ -827,13 +833,14 @@ void wf_trace(const WFParams W) {
           L.tri_end = L.tri_i;
         }
       }
+      bool needPop = false;  // one pop site per iteration (leaf taken, or no child entered)
       if (!finished && L.haveCur) {
         if (ref_is_leaf(L.cur)) {
           if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
             if (COUNT) { v_leaf++; v_park++; }
             L.tri_i = leaf_first(L.cur);
             L.tri_end = L.tri_i + leaf_count(L.cur);
-            L.haveCur = tl_pop(P, L, TS, cull);
+            needPop = true;
           }
         } else {
           if (COUNT) {
@@ -844,11 +851,12 @@ void wf_trace(const WFParams W) {
             }
           }
           const int sp0 = L.sp;
-          if (WIDE) tl_qnode(P, L, TS, cull);
+          if (WIDE) needPop = tl_qnode<false>(P, L, TS, cull);
           else tl_node(P, L, TS, cull);
           if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
         }
       }
+      if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
     }
     if (busy && finished) {
