@@ -555,11 +555,11 @@ RTD QLoad tl_qnode_load(const KParams& P, const TraceLane& L) {
   q.p[5] = ld<float4>(P.qnodes, off + (112 - L.offNz));
   return q;
 }
-RTD void tl_qnode_calc(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, const QLoad& q) {
+RTD bool tl_qnode_calc(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, const QLoad& q) {
   float k[4];
   int r[4];
   tl_qnode_keys(L, cull, P.cull_eps, q.rf, q.p[0], q.p[1], q.p[2], q.p[3], q.p[4], q.p[5], k, r);
-  tl_qnode_push(P, L, S, cull, k, r);
+  return tl_qnode_push<false>(P, L, S, cull, k, r);  // the caller pops
 }
 
 // start a ray on a lane whose origin, direction and anyhit are set: 1/d, plane offsets, root
@@ -653,17 +653,19 @@ RTD bool tl_dual_calc(const KParams& P, TraceLane& L, const TraceStack& TS, bool
     }
     if (finished) L.tri_end = L.tri_i;
   }
+  bool needPop = false;  // one pop site (as in wf_trace)
   if (!finished && L.haveCur) {
     if (!d.doNode) {  // a leaf: taken once the triangle cursor is free
       if (L.tri_i >= L.tri_end) {
         L.tri_i = leaf_first(L.cur);
         L.tri_end = L.tri_i + leaf_count(L.cur);
-        L.haveCur = tl_pop(P, L, TS, cull);
+        needPop = true;
       }
     } else {
-      tl_qnode_calc(P, L, TS, cull, d.q);
+      needPop = tl_qnode_calc(P, L, TS, cull, d.q);
     }
   }
+  if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
   return finished || (!L.haveCur && L.tri_i >= L.tri_end);
 }
 // the finisher's traversal step: both fetches first, then both tests, one memory round trip per
