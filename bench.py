@@ -241,71 +241,111 @@ def load_profile(config: str, W: int, H: int, F: int, slots: int):
 
 
 # wf_shade's algorithmic HBM bytes per path step (one path shaded in one bounce pass; rt_wavefront.h
-# shade_path, path-state layout DESIGN.md §3): a continuing path reads its active-list entry (4 B),
-# s5 (8), s0 + s2 (32), its two 8-B results (16) and its 24-B continuation ray = 84 B, and writes
-# s0 + s2 + s5 (40), the next continuation and shadow rays (48), two queue entries and an active
-# entry (12) = 100 B.  The s1/s3 rows (Lo, NEE, up to 64 B more) are left out: PF_ZLO paths skip
-# them.  So 184 B is a lower bound per path step; the count of path steps comes from the device
-# (rt_stats.path_steps: the active paths of every shade pass).
+# shade_path, path-state layout DESIGN.md §3), for a path that continues with a shadow ray and a
+# continuation.  Passes >= 2: it reads its active-list entry (4 B), s5 (8), s0 + s2 (32), its two
+# 8-B results (16) and its 24-B continuation ray = 84 B, and writes s0 + s2 + s5 (40), the next
+# continuation and shadow rays (2 x 24), two queue entries and an active entry (12) = 100 B.
+# Pass 0 (implicit camera paths): reads only the camera ray's 8-B result and writes the 16-B ray
+# records {d, s} of pass 1 (2 x 16) = 8 + 84 B.  Pass 1: reads the 16-B continuation record
+# instead of 24 B = 76 + 100 B.  The s1 / s3 / s4 rows (Lo, NEE, medium terms) are not counted
+# (PF_ZLO paths skip them), nor the final colour of finishing paths.  Path steps per pass come
+# from the device (rt_stats.pass0_steps / pass1_steps / path_steps; the finisher's steps,
+# rt_stats.finish_steps, run in wf_finish and are not wf_shade's).
 B_SHADE_STEP = 84 + 100
-B_SHADE_FINAL = 16    # the final colour of each sample (fin), blended later
+B_SHADE_P0 = 8 + 40 + 2 * 16 + 12
+B_SHADE_P1 = 76 + 100
+VALU_PEAK_G = N_SIMD * SPEC_CLOCK_GHZ / VALU_CYC  # G wave64-VALU-instructions/s (2 cycles each per SIMD)
 
 
-def roofline(st, vis, cnt, prof, trace_ms):
-    """wf_trace (the dominant kernel) priced against the HBM roofline (this path has no MFMA):
-    achieved = its algorithmic HBM bytes (the path-state stream it must move, B_RAY_*; the scene
-    is cache-resident) per launch / the launch time; traffic = rocprofv3 PMC HBM bytes per launch.
-    `limiter` names what actually bounds the kernel, from the measured utilisations: VALU issue at
-    the 2.4 GHz spec clock (standalone launch time of the PMC passes, kernels serialised), L2
-    bandwidth of its own traversal bytes, HBM.  `kernels.wf_shade`: the memory-bound shade against
-    the same HBM peak.  `reference_equivalent`: SURVEY §8(d)'s bytes of the reference's exhaustive
-    traversal, labelled as such and never used as frac."""
+def shade_bytes(st) -> float:
+    """wf_shade's algorithmic bytes over the counted path steps (see B_SHADE_*)."""
+    p0, p1 = st.get("pass0_steps", 0), st.get("pass1_steps", 0)
+    rest = max(0, st["path_steps"] - p0 - p1)
+    return B_SHADE_P0 * p0 + B_SHADE_P1 * p1 + B_SHADE_STEP * rest
+
+
+def trace_bytes(st) -> float:
+    """wf_trace's algorithmic HBM bytes over all its launches (B_RAY_*): camera rays (one per
+    sample), pass-1 rays (rt_stats.p1_rays) and the other secondary rays."""
+    cam, p1 = st["samples"], st.get("p1_rays", 0)
+    return B_RAY_SECONDARY * (st["rays"] - cam - p1) + B_RAY_PASS1 * p1 + B_RAY_CAMERA * cam
+
+
+def roofline(st, vis, cnt, prof, probe, steps):
+    """wf_trace, the dominant kernel, priced against the roofline of what bounds it.
+
+    Time per launch = the STANDALONE launch (`probe`: the same per-launch workload rendered as one
+    frame group, RT_FLAG_SERIAL, so no other kernel shares the CUs; HIP events on the launch
+    stream).  The timed region runs two frame groups whose launches overlap, so co-running per-launch
+    times would add up to more than the step (bench line `kernel`); this regime never does.
+    Utilisations at that time: HBM (algorithmic bytes: the path-state stream the kernel must move,
+    B_RAY_*; the ~25 MB scene stays in L2 / MALL), VALU issue (PMC VALU instructions per launch vs
+    1024 SIMDs x 2.4 GHz / 2 cycles) and L2 (its own traversal bytes).  `bound` is the largest of
+    them and achieved / peak / unit / frac are that roofline's; the others are given beside it
+    (`hbm`, `valu`, `l2`).  `traffic` = rocprofv3 PMC HBM bytes per launch.  `kernels.wf_shade`:
+    the memory-bound shade against the HBM peak.  `reference_equivalent`: SURVEY §8(d)'s bytes of
+    the reference's exhaustive traversal, labelled as such and never used as frac."""
     launches = max(1, st["trace_launches"])
     rays_l = st["rays"] / launches
-    cam_l = st["samples"] / launches                      # one camera ray per sample
-    p1_l = st.get("p1_rays", 0) / launches                # pass 1: 16-B ray records
-    alg = (B_RAY_SECONDARY * (rays_l - cam_l - p1_l) + B_RAY_PASS1 * p1_l + B_RAY_CAMERA * cam_l)
-    sec = trace_ms * 1e-3
-    out = {"bound": "hbm", "limiter": None, "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-           "kernel": "wf_trace", "avg_launch_ms": round(trace_ms, 4),
-           "avg_launch_ms_note": "HIP events on the launch stream during the timed steps (the other frame "
-                                 "group's wf_shade co-runs)",
-           "rays_per_launch": round(rays_l), "algorithmic_bytes_per_launch": round(alg),
-           "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "pass1": B_RAY_PASS1, "camera": B_RAY_CAMERA},
-           "pass1_rays_per_launch": round(p1_l)}
-    util = {"hbm": out["frac"]}
+    src = probe if (probe and probe.get("trace_launches")) else None
+    if src:
+        t_ms = src["trace_ms"] / src["trace_launches"]
+        alg = trace_bytes(src) / src["trace_launches"]
+        regime = (f"standalone: the probe render of {src.get('frames')} frames as one frame group (RT_FLAG_SERIAL), "
+                  f"{src['trace_launches']} launches, HIP events on the launch stream")
+    else:  # no probe: the co-running launches (labelled)
+        t_ms = st["trace_ms"] / launches
+        alg = trace_bytes(st) / launches
+        regime = "co-running (two frame groups overlap; per-launch times add up to more than the step)"
+    sec = t_ms * 1e-3
+    hbm = {"achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": round(alg),
+           "algorithmic_bytes_per_ray": {"secondary": B_RAY_SECONDARY, "pass1": B_RAY_PASS1, "camera": B_RAY_CAMERA}}
+    out = {"bound": "hbm", "achieved": hbm["achieved"], "peak": hbm["peak"], "unit": hbm["unit"], "frac": hbm["frac"],
+           "traffic": None, "kernel": "wf_trace", "avg_launch_ms": round(t_ms, 4), "avg_launch_ms_regime": regime,
+           "launches_per_step": round(launches / max(1, steps), 2),
+           "rays_per_launch": round(src["rays"] / src["trace_launches"]) if src else round(rays_l),
+           "hbm": hbm}
+    util = {"hbm": hbm["frac"]}
     pt = (prof or {}).get("kernels", {}).get("wf_trace")
     if pt:
         out["traffic"] = pt.get("hbm_bytes_per_launch")
         out["profile"] = prof["_file"]
-        out["profile_avg_launch_ms"] = pt.get("avg_launch_ms")
-        sa = pt.get("avg_launch_ms_standalone")
-        out["avg_launch_ms_standalone"] = sa
+        out["profile_avg_launch_ms_standalone"] = pt.get("probe_avg_launch_ms") or pt.get("avg_launch_ms_standalone")
+        out["profile_avg_launch_ms_corunning"] = pt.get("avg_launch_ms")
         sq = pt.get("SQ", {})
-        if sq.get("SQ_INSTS_VALU") and sa:
-            issue = sq["SQ_INSTS_VALU"] * VALU_CYC / (N_SIMD * SPEC_CLOCK_GHZ * 1e9 * sa * 1e-3)
-            v = {"insts_per_launch": round(sq["SQ_INSTS_VALU"]), "insts_per_ray": round(sq["SQ_INSTS_VALU"] / rays_l, 1),
-                 "cycles_per_inst": VALU_CYC, "issue_frac_at_spec_clock": round(issue, 4),
+        if sq.get("SQ_INSTS_VALU"):
+            ach = sq["SQ_INSTS_VALU"] / sec / 1e9
+            v = {"achieved": round(ach, 1), "peak": round(VALU_PEAK_G, 1), "unit": "G VALU wave-instr/s",
+                 "frac": round(ach / VALU_PEAK_G, 4), "insts_per_launch": round(sq["SQ_INSTS_VALU"]),
+                 "insts_per_ray": round(sq["SQ_INSTS_VALU"] / rays_l, 1), "cycles_per_inst": VALU_CYC,
                  "spec_clock_ghz": SPEC_CLOCK_GHZ}
+            if sq.get("SQ_INSTS_SALU"):
+                v["salu_per_ray"] = round(sq["SQ_INSTS_SALU"] / rays_l, 1)
+                v["salu_per_valu"] = round(sq["SQ_INSTS_SALU"] / sq["SQ_INSTS_VALU"], 3)
             if pt.get("effective_clock_ghz"):
                 v["effective_clock_ghz"] = pt["effective_clock_ghz"]
-                v["issue_frac_at_effective_clock"] = round(issue * SPEC_CLOCK_GHZ / pt["effective_clock_ghz"], 4)
             if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("SQ_THREAD_CYCLES_VALU"):
                 v["lane_util"] = round(sq["SQ_THREAD_CYCLES_VALU"] / (64 * sq["SQ_ACTIVE_INST_VALU"]), 4)
             if pt.get("wave_cycle_split"):
                 v["wave_cycle_split"] = pt["wave_cycle_split"]
             out["valu"] = v
-            util["valu_issue"] = v["issue_frac_at_spec_clock"]
+            util["valu_issue"] = v["frac"]
     if vis and vis.get("rays"):
         own = (B_QNODE * vis["internal_pops"] + B_TRI_REC * vis["tri_tests"]) / vis["rays"]
-        t_l2 = (out.get("avg_launch_ms_standalone") or trace_ms) * 1e-3
-        out["l2"] = {"own_traversal_bytes_per_ray": round(own, 1),
-                     "achieved": round(own * rays_l / t_l2 / 1e9, 1), "peak": L2_PEAK_GBS,
-                     "frac": round(own * rays_l / t_l2 / 1e9 / L2_PEAK_GBS, 4)}
+        rl = src["rays"] / src["trace_launches"] if src else rays_l
+        out["l2"] = {"own_traversal_bytes_per_ray": round(own, 1), "achieved": round(own * rl / sec / 1e9, 1),
+                     "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": round(own * rl / sec / 1e9 / L2_PEAK_GBS, 4)}
         util["l2"] = out["l2"]["frac"]
-    out["limiter"] = max(util, key=util.get)
+    lim = max(util, key=util.get)
     out["utilisation"] = util
+    out["limiter"] = lim
+    if lim == "valu_issue":
+        v = out["valu"]
+        out.update(bound="valu_issue", achieved=v["achieved"], peak=v["peak"], unit=v["unit"], frac=v["frac"])
+    elif lim == "l2":
+        l2 = out["l2"]
+        out.update(bound="l2", achieved=l2["achieved"], peak=l2["peak"], unit=l2["unit"], frac=l2["frac"])
     if cnt:
         per_ray = (B_INT * cnt["internal_pops"] + B_LEAF * cnt["leaf_pops"] + B_TRI * cnt["tri_tests"] +
                    B_UPD * cnt["closer_updates"]) / cnt["rays"]
@@ -315,9 +355,7 @@ def roofline(st, vis, cnt, prof, trace_ms):
                     "ray traced here; the device traversal visits fewer nodes, so this is not a bandwidth"}
     ps = (prof or {}).get("kernels", {}).get("wf_shade")
     if ps and ps.get("avg_launch_ms_standalone") and st.get("path_steps"):
-        shade_launches = max(1, st["trace_launches"])  # one wf_shade per wf_trace launch
-        steps_l = st["path_steps"] / shade_launches
-        alg_s = B_SHADE_STEP * steps_l + B_SHADE_FINAL * st["samples"] / shade_launches
+        alg_s = shade_bytes(st) / launches  # one wf_shade per wf_trace launch
         t_s = ps["avg_launch_ms_standalone"] * 1e-3
         out["kernels"] = {"wf_shade": {
             "bound": "hbm", "achieved": round(alg_s / t_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -325,10 +363,13 @@ def roofline(st, vis, cnt, prof, trace_ms):
             "traffic_frac": (round(ps["hbm_bytes_per_launch"] / t_s / 1e9 / HBM_PEAK_GBS, 4)
                              if ps.get("hbm_bytes_per_launch") else None),
             "avg_launch_ms_standalone": ps["avg_launch_ms_standalone"],
-            "avg_launch_ms_corunning": ps.get("avg_launch_ms"),
-            "algorithmic_bytes_per_path_step": B_SHADE_STEP, "path_steps_per_launch": round(steps_l),
-            "note": "algorithmic bytes = a lower bound of the path-state rows a step moves (184 B/path step, "
-                    "s1/s3 rows excluded); time = the PMC passes' standalone launches (kernels serialised)",
+            "launches_per_step": round(launches / max(1, steps), 2),
+            "algorithmic_bytes_per_launch": round(alg_s),
+            "algorithmic_bytes_per_path_step": {"pass0": B_SHADE_P0, "pass1": B_SHADE_P1, "later": B_SHADE_STEP},
+            "path_steps_per_launch": round(st["path_steps"] / launches),
+            "note": "algorithmic bytes of a continuing path's step (s1/s3/s4 rows and final colours not counted); "
+                    "time = the PMC passes' standalone launches (dispatches serialised), the visit-count frame's "
+                    "launches excluded",
             "profile": prof["_file"]}}
     return out
 
@@ -380,13 +421,22 @@ def dry_run(args, rank: int, world: int) -> int:
         ok = rank != 0 or all(int(p[0, 0]) == r for r, p in enumerate(parts))
     else:
         total_px, ok, elapsed = px, True, torch.tensor([time.perf_counter() - t0])
+    rank_ms = [round(float(elapsed[0]) * 1e3, 3)] * world
+    if world > 1:  # each rank's own time (the same all-gather the GPU run's line uses)
+        mine = torch.tensor([(time.perf_counter() - t0) * 1e3], dtype=torch.float64)
+        everyone = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(everyone, mine)
+        rank_ms = [round(float(t[0]), 3) for t in everyone]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": steps,
                           "warmup": warm, "dry_run": True, "frames_planned": total_frames,
                           "rand_origin_last": float(ro[-1]), "pixels_covered": total_px,
                           "frame_pixels": W * H, "gather_ok": bool(ok),
                           "tile_assignment": "modulo" if owner is None else "cost-balanced",
-                          "gather_ms": round(float(elapsed[0]) * 1e3, 3)}), flush=True)
+                          "gather_ms": round(float(elapsed[0]) * 1e3, 3),
+                          "collective": {"backend": dist.get_backend() if world > 1 else None, "world": world,
+                                         "gather_ms": round(float(elapsed[0]) * 1e3, 3), "rank_ms": rank_ms}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0 if (total_px == W * H and ok) else 1
@@ -473,12 +523,18 @@ def main(argv=None) -> int:
     gathered = torch.empty(world * nfloat, dtype=torch.float32, device="cuda") if rank == 0 else None
     frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
 
+    gather_ev = []  # (start, end) CUDA events around each step's frame-end gather on this rank's stream
+
     def step(k: int) -> None:
         r.render_async(fp, ro[k * F:(k + 1) * F])
         if args.no_gather:
             return
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        gather_ev.append(ev)
+        ev[0].record()  # (runs once this step's render has finished: same stream)
         if world == 1:
             r.assemble_frame(ad["ptr"], 1, frame.data_ptr())
+            ev[1].record()
             return
         r.copy_accum_device(local.data_ptr(), ad["bytes"])
         if args.rehearse:  # gloo: host copies
@@ -491,6 +547,7 @@ def main(argv=None) -> int:
             dist.gather(local, gather_list=parts, dst=0)
         if rank == 0:
             r.assemble_frame(gathered.data_ptr(), world, frame.data_ptr())
+        ev[1].record()  # (the current stream waited for the collective's stream: async_op=False)
 
     t_w = time.perf_counter()
     for k in range(warm):
@@ -499,6 +556,7 @@ def main(argv=None) -> int:
     if rank == 0:
         print(f"bench: warmup {warm} x {F} frames in {time.perf_counter() - t_w:.1f} s", file=sys.stderr, flush=True)
     r.reset_stats()
+    gather_ev.clear()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -510,17 +568,42 @@ def main(argv=None) -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = r.stats()
+    gather_ms = (sum(a.elapsed_time(b) for a, b in gather_ev) / len(gather_ev)) if gather_ev else 0.0
+    rank_elapsed = elapsed
 
     # whole-job aggregates
     vals = torch.tensor([elapsed, float(st["rays"]), float(st["samples"])], dtype=torch.float64, device=cdev)
+    per_rank = torch.tensor([rank_elapsed * 1e3 / max(1, steps), gather_ms], dtype=torch.float64, device=cdev)
     if dist:
         t_max = vals[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         sums = vals[1:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         elapsed, rays, samples = float(t_max[0]), float(sums[0]), float(sums[1])
+        everyone = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(everyone, per_rank)
+        rank_rows = [[float(x) for x in t.cpu()] for t in everyone]
     else:
         rays, samples = float(st["rays"]), float(st["samples"])
+        rank_rows = [[float(x) for x in per_rank.cpu()]]
+    collective = {"backend": dist.get_backend() if dist else None, "world": dist.get_world_size() if dist else 1,
+                  "rehearsal": bool(args.rehearse),
+                  "gather_ms": round(rank_rows[0][1], 3),  # rank 0: copy + gather + un-permute, per step
+                  "gather_ms_per_rank": [round(x[1], 3) for x in rank_rows],
+                  "rank_ms": [round(x[0], 3) for x in rank_rows],  # each rank's timed wall time per step
+                  "rank_max_over_mean": round(max(x[0] for x in rank_rows) / (sum(x[0] for x in rank_rows) / len(rank_rows)), 4)}
+
+    # standalone wf_trace launches for the roofline (outside the timed region): the same frame-group
+    # workload as one timed launch (frames per group = F / (batches x 2)), run as ONE group
+    # (RT_FLAG_SERIAL), so no other kernel shares the CUs; HIP events on the launch stream
+    probe = None
+    if st["trace_launches"]:
+        from rtamd.renderer import RT_FLAG_SERIAL
+        per_group = max(1, round(F * (fp.max_bounce + 1) * steps / st["trace_launches"]))
+        r.reset_stats()
+        r.render(cf.frame_params(W, H, flags=RT_FLAG_SERIAL), ro[-1 - per_group:-1])
+        probe = r.stats()
+        probe["frames"] = per_group
 
     frame_sha = None
     if args.frame_sha and rank == 0 and frame is not None and not args.no_gather:
@@ -557,7 +640,8 @@ def main(argv=None) -> int:
             lat.append(time.perf_counter() - t2)
         single["ms_single_frame_latency"] = round(float(np.median(lat)) * 1e3, 3)
 
-    # own-traversal visit counts (one extra frame, outside the timed region)
+    # own-traversal visit counts (one extra frame, outside the timed region; tools/summarize_profile.py
+    # drops the launches from this frame on)
     r.reset_stats()
     r.render(cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS), ro[-1:])
     vis = r.stats()
@@ -595,9 +679,15 @@ def main(argv=None) -> int:
                    "tile_assignment": "cost-balanced (rt_tile_costs probe frame)" if balanced else "interleaved t % N",
                    "steps_in_flight": args.pipeline if pipelined else 1,
                    "triangles": sd.counts["n_triangles"], "bvh_nodes": sd.counts["n_nodes"]},
-        "kernel": {"name": "wf_trace", "avg_launch_ms": round(trace_ms, 4), "launches": st["trace_launches"],
+        "kernel": {"name": "wf_trace", "launches": st["trace_launches"],
                    "render_call_ms": round(launch_ms, 4), "render_calls": st["launches"],
-                   "trace_share": round(st["trace_ms"] / max(1e-9, st["kernel_ms"]), 4)},
+                   # two frame groups on two streams: their launches overlap, so per-launch durations
+                   # measured co-running add up to more than the step; the union of the launches'
+                   # intervals is the time during which any traversal ran
+                   "corunning_avg_launch_ms": round(trace_ms, 4),
+                   "busy_ms_per_step": round(st.get("trace_busy_ms", 0.0) / max(1, steps), 3),
+                   "busy_share_of_step": round(st.get("trace_busy_ms", 0.0) / max(1e-9, elapsed * 1e3), 4)},
+        "collective": collective,
         "parity": "bit-exact vs oracle (tests/test_gpu_parity.py)",
     }
     if frame_sha:
@@ -614,7 +704,7 @@ def main(argv=None) -> int:
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"], cnt = cpu_baseline(sd, env, W, H, fp, args.cpu_seconds, args.cpu_threads)
     prof = load_profile(args.config, W, H, F, path_slots)
-    out["roofline"] = roofline(st, vis, cnt, prof, trace_ms)
+    out["roofline"] = roofline(st, vis, cnt, prof, probe, steps)
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -35,6 +35,13 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* ABI version of this header.  4: rt_stats gained pass0_steps, pass1_steps, finish_steps and
+ * trace_busy_ms (round 4; round 3 had added path_steps and p1_rays), and rt_stats_get_sized /
+ * rt_abi_version / RT_FLAG_SERIAL appeared.  A binding built against an
+ * older header calls rt_stats_get_sized with its own sizeof(rt_stats), or checks rt_abi_version()
+ * at load time. */
+#define RT_ABI_VERSION 4
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -99,7 +106,9 @@ enum {
   RT_FLAG_COUNT_VISITS = 2,       /* also count node/triangle visits (slower)                  */
   RT_FLAG_MEGAKERNEL = 4,         /* single persistent megakernel instead of the wavefront path */
   RT_FLAG_NO_FINISH = 8,          /* never end paths in the path-persistent finisher            */
-  RT_FLAG_FINISH = 16             /* use the finisher whatever the batch size (rt_set_finish)   */
+  RT_FLAG_FINISH = 16,            /* use the finisher whatever the batch size (rt_set_finish)   */
+  RT_FLAG_SERIAL = 32             /* measurement: one frame group per batch (no two groups' kernels
+                                     overlap), at most one group's path state of frames per batch */
 };
 
 typedef struct rt_stats {
@@ -112,8 +121,15 @@ typedef struct rt_stats {
   double trace_ms;          /* summed duration of those launches (HIP events around each) */
   uint64_t trace_iters;     /* RT_FLAG_COUNT_VISITS: traversal loop iterations, all waves */
   uint64_t trace_iters_max; /* RT_FLAG_COUNT_VISITS: max loop iterations of one wave       */
-  uint64_t path_steps;      /* wavefront path: shade steps (one per path per bounce pass)  */
+  uint64_t path_steps;      /* wavefront path: wf_shade steps (one per path per bounce pass) */
   uint64_t p1_rays;         /* wavefront path: rays traced from pass 0's 16-B ray records  */
+  /* ---- ABI 4 */
+  uint64_t pass0_steps;     /* of path_steps: pass 0 (implicit camera paths)                */
+  uint64_t pass1_steps;     /* of path_steps: pass 1 (paths whose rays are 16-B records)    */
+  uint64_t finish_steps;    /* shade steps run by the path-persistent finisher (wf_finish)  */
+  double trace_busy_ms;     /* union of the traversal launches' intervals: the time during
+                               which at least one of them ran (frame groups overlap, so
+                               trace_ms can exceed it)                                       */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;
@@ -187,8 +203,11 @@ int rt_render_async(rt_ctx* ctx, const rt_frame_params* params, const float* ran
 int rt_render(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
               rt_stats* stats);
 int rt_synchronize(rt_ctx* ctx);
-int rt_stats_get(rt_ctx* ctx, rt_stats* stats);  /* synchronises */
+int rt_stats_get(rt_ctx* ctx, rt_stats* stats);  /* synchronises; writes sizeof(rt_stats) of ABI 4 */
+/* The same, writing at most stats_bytes bytes (a caller's own, possibly older, sizeof(rt_stats)). */
+int rt_stats_get_sized(rt_ctx* ctx, rt_stats* stats, size_t stats_bytes);
 int rt_stats_reset(rt_ctx* ctx);
+int rt_abi_version(void);                        /* RT_ABI_VERSION the library was built with */
 
 /* The HIP stream (hipStream_t) the ctx launches on, for external events / collectives. */
 int rt_get_stream(const rt_ctx* ctx, void** stream);

@@ -67,13 +67,16 @@ struct __attribute__((aligned(16))) GNode {
   int4 ref;   // left ref, right ref, -, -
 };
 // 4-wide node collapsed from the binary tree above (same exact fp32 child boxes, SoA: child k
-// in component k; an empty slot has NaN bounds, which the slab test never hits).  128 B = one
-// cache line; one fetch replaces about two dependent binary steps.
+// in component k; an empty slot has the inverted bounds lo = +inf, hi = -inf, which the slab test
+// never hits).  128 B = one cache line; one fetch replaces about two dependent binary steps.
+// ord[o]: the fast traversal's child order for ray-direction octant o (bit a: direction component
+// a negative): nibble c = the set of children that come after child c in that order.
 struct __attribute__((aligned(16))) QNode {
   float4 lox, loy, loz, hix, hiy, hiz;
   int4 ref;  // child refs (QNode index or leaf ref), Q_EMPTY for an empty slot
-  int4 pad;
+  uint16_t ord[8];
 };
+static_assert(sizeof(QNode) == 128, "one cache line");
 constexpr int Q_EMPTY = 0x7fffffff;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 RTD bool ref_is_leaf(int r) { return ((uint32_t)r & LEAF_BIT) != 0u; }

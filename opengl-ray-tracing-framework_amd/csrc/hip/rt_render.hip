@@ -57,6 +57,7 @@ struct rt_ctx {
     bool valid = false;
     float angle = 0.0f;                       // the envAngle d was built for
     hipEvent_t last_use = nullptr;            // on the ctx stream after the last call that read d
+    hipEvent_t built = nullptr;               // after the kernel that last built d (on that call's stream)
   };
   LightTable light[2];
   int light_cur = 0;                          // the table the last call used
@@ -75,6 +76,11 @@ struct rt_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> trace_events;  // traversal launches
   std::vector<hipEvent_t> event_pool;
   double kernel_ms = 0.0, trace_ms = 0.0;
+  // union of the traversal launches' intervals (rt_stats.trace_busy_ms): start / end of each launch
+  // relative to t_ref (recorded on the ctx stream at creation and at every rt_stats_reset, with
+  // nothing in flight), kept as sorted disjoint intervals
+  hipEvent_t t_ref = nullptr;
+  std::vector<std::pair<double, double>> busy;
   uint64_t launches = 0, trace_launches = 0;
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
@@ -89,6 +95,7 @@ struct rt_ctx {
   };
   FrameTable ft[5];
   int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
+  bool fast_trace = false;                    // wf_trace MODE_FAST + MODE_SLOWIN (dev: RT_FAST_TRACE=0, the exact kernel alone)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
@@ -501,13 +508,36 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     }
     int refs[4] = {rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY};
     for (size_t i = 0; i < sl.size(); i++) refs[i] = is_leaf(sl[i].ref) ? sl[i].ref : build(sl[i].ref, depth + 1);
-    const float qnan = std::nanf("");
+    // an empty slot is the inverted box lo = +inf, hi = -inf: for every finite 1/d its entry t0 is
+    // +inf and its exit t1 -inf (and for a zero component the literal slab leaves the other axes
+    // deciding), so no slab test ever hits it
+    const float pinf = INFINITY;
     float lo[3][4], hi[3][4];
     for (int k = 0; k < 3; k++)
       for (int i = 0; i < 4; i++) {
-        lo[k][i] = i < (int)sl.size() ? sl[i].lo[k] : qnan;
-        hi[k][i] = i < (int)sl.size() ? sl[i].hi[k] : qnan;
+        lo[k][i] = i < (int)sl.size() ? sl[i].lo[k] : pinf;
+        hi[k][i] = i < (int)sl.size() ? sl[i].hi[k] : -pinf;
       }
+    // fast traversal's child order per ray-direction octant o (bit a set: component a of the
+    // direction negative): children by the projection of their box centre onto the octant's
+    // diagonal, nearest first; ord[o] holds, in nibble c, the children that come after child c
+    uint16_t ord[8];
+    for (int o = 0; o < 8; o++) {
+      double key[4];
+      for (int i = 0; i < 4; i++) {
+        key[i] = HUGE_VAL;
+        if (i < (int)sl.size()) {
+          key[i] = 0.0;
+          for (int k = 0; k < 3; k++)
+            key[i] += (((o >> k) & 1) ? -0.5 : 0.5) * ((double)sl[i].lo[k] + (double)sl[i].hi[k]);
+        }
+      }
+      uint32_t m = 0;
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+          if (j != i && (key[j] > key[i] || (key[j] == key[i] && j > i))) m |= 1u << (4 * i + j);
+      ord[o] = (uint16_t)m;
+    }
     rtd::QNode& q = qn[idx];
     q.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     q.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
@@ -516,7 +546,7 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     q.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
     q.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
     q.ref = make_int4(refs[0], refs[1], refs[2], refs[3]);
-    q.pad = make_int4((int)sl.size(), 0, 0, 0);
+    memcpy(&q.ord, ord, sizeof(ord));
     return idx;
   };
   qroot = is_leaf(croot) ? croot : build(croot, 1);
@@ -581,6 +611,11 @@ int occupancy(rt_ctx* c) {
     const hipError_t e =
         cam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, true>, 256, c->trace_lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, false>, 256, c->trace_lds);
+    int bf = b;  // the fast instantiation runs on the same grid
+    const hipError_t ef =
+        cam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&bf, rtd::wf_trace<false, true, true, false, false, rtd::MODE_FAST>, 256, c->trace_lds)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&bf, rtd::wf_trace<false, true, false, false, false, rtd::MODE_FAST>, 256, c->trace_lds);
+    if (ef == hipSuccess && c->fast_trace) b = std::min(b, bf);
     return e == hipSuccess ? std::max(1, b) : 1;
   };
   c->trace_bpc0 = occ(true);  // pass 0 is the implicit camera pass
@@ -622,6 +657,24 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
   // pass 1 reads the 16-B rays pass 0 queued (WFState::org) in an instantiation of its own, so the
   // later passes' kernel carries none of it
   const bool p1 = !WP.cam_n && WP.pass == 1 && WP.p1_compact;
+  if (!COUNT && WIDE && c->fast_trace) {
+    // fast traversal, then the exact kernel over the rays it deferred (zero direction components,
+    // exact distance ties: usually none, and its blocks exit at once)
+    constexpr int F = rtd::MODE_FAST, SL = rtd::MODE_SLOWIN;
+    if (small) {  // static first shares of mid-size passes
+      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+    } else {
+      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+    }
+    if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    return;
+  }
   if (small && !COUNT && WIDE) {  // static first shares of mid-size passes
     if (WP.cam_n)
       hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
@@ -665,18 +718,46 @@ hipEvent_t take_event(rt_ctx* c) {
 // Timing events of launches not yet folded into kernel_ms / trace_ms: a front end that never
 // calls rt_synchronize (it waits on its own stream or events) would otherwise grow these lists
 // without bound.  Past `cap` pending pairs, the oldest are waited for, folded and recycled.
-int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap) {
+// a finished launch's (start, end) events: its duration into acc_ms and, for traversal launches
+// (busy), its interval into the union c->busy
+int fold_pair(rt_ctx* c, const std::pair<hipEvent_t, hipEvent_t>& e, double& acc_ms, bool busy) {
+  float ms = 0.0f;
+  HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
+  acc_ms += ms;
+  if (busy && c->t_ref) {
+    float a = 0.0f, b = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&a, c->t_ref, e.first));
+    HIPCHK(c, hipEventElapsedTime(&b, c->t_ref, e.second));
+    double lo = a, hi = std::max(a, b);
+    auto& v = c->busy;
+    // merge [lo, hi] into the sorted disjoint list (launches arrive nearly in time order)
+    auto it = std::upper_bound(v.begin(), v.end(), std::make_pair(lo, hi));
+    if (it != v.begin() && std::prev(it)->second >= lo) {
+      --it;
+      lo = it->first;
+      hi = std::max(hi, it->second);
+      it = v.erase(it);
+    }
+    while (it != v.end() && it->first <= hi) {
+      hi = std::max(hi, it->second);
+      it = v.erase(it);
+    }
+    v.insert(it, std::make_pair(lo, hi));
+  }
+  c->event_pool.push_back(e.first);
+  c->event_pool.push_back(e.second);
+  return RT_OK;
+}
+
+int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap, bool busy) {
   if (ev.size() <= cap) return RT_OK;
   const size_t n = ev.size() - cap / 2;
   for (size_t i = 0; i < n; i++) {
     // pairs of one call can sit on different streams (frame / pixel groups, pipelined sets), so
     // each pair is waited for itself (in queue order: cheap once the first is done)
     HIPCHK(c, hipEventSynchronize(ev[i].second));
-    float ms = 0.0f;
-    HIPCHK(c, hipEventElapsedTime(&ms, ev[i].first, ev[i].second));
-    acc_ms += ms;
-    c->event_pool.push_back(ev[i].first);
-    c->event_pool.push_back(ev[i].second);
+    const int rc = fold_pair(c, ev[i], acc_ms, busy);
+    if (rc) return rc;
   }
   ev.erase(ev.begin(), ev.begin() + (ptrdiff_t)n);
   return RT_OK;
@@ -756,8 +837,10 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = knob("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
+  if (const char* e = knob("RT_FAST_TRACE")) c->fast_trace = atoi(e) != 0;
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess || hipEventCreate(&c->t_ref) != hipSuccess ||
+      hipEventRecord(c->t_ref, c->stream) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -773,10 +856,12 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
+  if (c->t_ref) (void)hipEventDestroy(c->t_ref);
   dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trx); dfree(c->d_trin); dfree(c->d_mats);
   for (auto& t : c->light) {
     dfree(t.d);
     if (t.last_use) (void)hipEventDestroy(t.last_use);
+    if (t.built) (void)hipEventDestroy(t.built);
   }
   dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
   for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -1205,7 +1290,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   static const bool pix_ok = !knob("RT_PIX_SPLIT") || atoi(knob("RT_PIX_SPLIT")) != 0;
   const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
   const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
-  bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && n_trace_pre > 0 &&
+  const bool serial = (fp->flags & RT_FLAG_SERIAL) != 0 && !(fp->flags & RT_FLAG_MEGAKERNEL);
+  bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && !serial && n_trace_pre > 0 &&
               c->n_valid >= 64 * c->n_groups && !c->tile_cost_on &&
               (n_trace_pre < c->n_groups ||
                (n_trace_pre <= c->frames_cap && (size_t)n_trace_pre * nv < c->pipe_nomem_slots));
@@ -1332,16 +1418,24 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         hipLaunchKernelGGL(rtd::rt_light_table_kernel, dim3(std::max(1u, std::min(4096u, (n + 255) / 256))), dim3(256),
                            0, ps, E, LT->d);
         HIPCHK(c, hipGetLastError());
+        if (!LT->built) HIPCHK(c, hipEventCreateWithFlags(&LT->built, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(LT->built, ps));
         LT->angle = fp->env_angle;
         LT->valid = true;
       }
     }
+    // every call that reads the table waits for its build, which may still run on another call's
+    // stream (a pipelined call on aux[1] rebuilt it; this one runs on aux[2] with the same angle)
+    if (LT->built) HIPCHK(c, hipStreamWaitEvent(ps, LT->built, 0));
   }
   int done = 0;
   while (done < n_traced) {
     KParams P;
     memset(&P, 0, sizeof(P));
-    const int cap = (fp->flags & RT_FLAG_MEGAKERNEL) ? RT_MAX_FRAMES_PER_LAUNCH : c->frames_cap;
+    // RT_FLAG_SERIAL: one frame group per batch, as many frames as one group's path state holds
+    const int cap = (fp->flags & RT_FLAG_MEGAKERNEL) ? RT_MAX_FRAMES_PER_LAUNCH
+                    : serial ? (int)std::max<size_t>(1, std::min<size_t>((size_t)c->frames_cap, c->wf_paths / nv))
+                             : c->frames_cap;
     const int nf = std::min(cap, n_traced - done);
     P.loop_num = d_loop + done;
     P.rand_origin = d_ro + done;
@@ -1404,8 +1498,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       // of fewer frames than groups (one frame per call: the reference's own usage) is split by
       // pixels instead (work items [w0, w1) each, all frames), so the groups' latency-bound late
       // passes still overlap each other
-      const bool pix_split = !pipe && pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
-      const int G = pipe ? 1 : pix_split ? c->n_groups : std::min(c->n_groups, nf);
+      const bool pix_split = !pipe && !serial && pix_ok && nf < c->n_groups && c->n_valid >= 64 * c->n_groups && !c->tile_cost_on;
+      const int G = (pipe || serial) ? 1 : pix_split ? c->n_groups : std::min(c->n_groups, nf);
       const unsigned int trace_grid = (unsigned)(c->n_cus * std::max(c->trace_bpc, c->trace_bpc0));
       const unsigned int trace_grid0 = (unsigned)(c->n_cus * c->trace_bpc0);
       const unsigned int trace_grid1 = (unsigned)(c->n_cus * c->trace_bpc);
@@ -1705,8 +1799,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     HIPCHK(c, hipEventRecord(LT->last_use, c->stream));
     c->events.push_back({e0, e1});
     c->launches++;
-    int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents);
-    if (!frc) frc = fold_events(c, c->events, c->kernel_ms, kMaxPendingEvents);
+    int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents, true);
+    if (!frc) frc = fold_events(c, c->events, c->kernel_ms, kMaxPendingEvents, false);
     if (frc) return frc;
   }
   return RT_OK;
@@ -1716,22 +1810,28 @@ int rt_synchronize(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  // (the stream joins every group and pipelined set of each call, so all pairs have finished)
   for (auto& e : c->events) {
-    float ms = 0.0f;
-    HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
-    c->kernel_ms += ms;
-    c->event_pool.push_back(e.first);
-    c->event_pool.push_back(e.second);
+    const int rc = fold_pair(c, e, c->kernel_ms, false);
+    if (rc) return rc;
   }
   c->events.clear();
   for (auto& e : c->trace_events) {
-    float ms = 0.0f;
-    HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
-    c->trace_ms += ms;
-    c->event_pool.push_back(e.first);
-    c->event_pool.push_back(e.second);
+    const int rc = fold_pair(c, e, c->trace_ms, true);
+    if (rc) return rc;
   }
   c->trace_events.clear();
+  return RT_OK;
+}
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_stats_get_sized(rt_ctx* c, rt_stats* st, size_t bytes) {
+  if (!c || !st) return RT_ERR_ARG;
+  rt_stats full;
+  const int rc = rt_stats_get(c, &full);
+  if (rc) return rc;
+  memcpy(st, &full, std::min(bytes, sizeof(full)));
   return RT_OK;
 }
 
@@ -1739,6 +1839,7 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   if (!c || !st) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
+  memset(st, 0, sizeof(*st));
   unsigned long long h[8];
   HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
   st->rays = h[0]; st->samples = h[1]; st->internal_pops = h[2]; st->leaf_pops = h[3]; st->tri_tests = h[4];
@@ -1748,10 +1849,16 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->trace_ms = c->trace_ms;
   st->trace_iters = h[5];
   st->trace_iters_max = h[6];
-  unsigned long long ps[2] = {0, 0};
+  unsigned long long ps[5] = {0, 0, 0, 0, 0};
   HIPCHK(c, hipMemcpy(ps, c->d_stats + 16, sizeof(ps), hipMemcpyDeviceToHost));
   st->path_steps = ps[0];
   st->p1_rays = ps[1];
+  st->pass0_steps = ps[2];
+  st->pass1_steps = ps[3];
+  st->finish_steps = ps[4];
+  double busy = 0.0;
+  for (const auto& iv : c->busy) busy += iv.second - iv.first;
+  st->trace_busy_ms = busy;
   return RT_OK;
 }
 
@@ -1764,6 +1871,8 @@ int rt_stats_reset(rt_ctx* c) {
   c->launches = 0;
   c->trace_ms = 0.0;
   c->trace_launches = 0;
+  c->busy.clear();
+  if (c->t_ref) HIPCHK(c, hipEventRecord(c->t_ref, c->stream));  // nothing in flight (synchronised)
   return RT_OK;
 }
 

@@ -280,6 +280,9 @@ struct TraceLane {
   RTD float limit(float eps) const { return cull_limit(best, eps, ix, iy, iz); }
   int besttri, sp, cur, tri_i, tri_end;
   int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
+  // fast traversal: the near-plane offsets packed in bytes 0-2 (far = near ^ 48 / 80 / 112) and
+  // 2 x the octant of d in byte 3 (QNode::ord[octant] at 112 + that)
+  uint32_t offPk;
   bool haveCur, anyhit, finite;
 };
 
@@ -292,11 +295,23 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;  // {ref, key
 RTD unsigned long long pack_ent(int2 e) { return (unsigned long long)(uint32_t)e.x | ((unsigned long long)(uint32_t)e.y << 32); }
 RTD int2 unpack_ent(unsigned long long v) { return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32)); }
 constexpr int TL_LANES = 256;
+RTD uint32_t lds_addr(const void* p) { return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p; }
 struct TraceStack {
-  int2* lds;
-  gu64* ovf;
+  int2* lds;      // this lane's column: entry j at lds[j * TL_LANES]
+  int2* lds0;     // the block's stack (lane 0's column)
+  gu64* ovf;      // the block's overflow columns: entry j >= KL of block lane l at ovf[(j - KL) * ovs + l]
   unsigned ovs;
   int KL;
+  RTD uint32_t lane() const {
+    uint32_t l = (lds_addr(lds) - lds_addr(lds0)) >> 3;
+    asm volatile("" : "+v"(l));  // recomputed where used: a hoisted 64-bit address would live in scratch
+    return l;
+  }
+  // the overflow slot of entry j (the lane from the LDS column: no 64-bit per-lane pointer lives
+  // across the traversal loop)
+  RTD gu64* ovf_at(int j) const { return ovf + (size_t)(j - KL) * ovs + lane(); }
+  // the lane's current queue entry, kept in LDS after the stack (one VGPR less across the loop)
+  RTD int* entry_slot() const { return reinterpret_cast<int*>(lds0 + KL * TL_LANES) + lane(); }
 };
 
 // byte-offset loads from a uniform base: the compiler emits the saddr form (32-bit lane offset)
@@ -388,7 +403,7 @@ RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
 
 RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
   if (L.sp < S.KL) S.lds[L.sp * TL_LANES] = ent;
-  else S.ovf[(size_t)(L.sp - S.KL) * S.ovs] = pack_ent(ent);
+  else *S.ovf_at(L.sp) = pack_ent(ent);
   ++L.sp;
 }
 
@@ -397,7 +412,7 @@ RTD bool tl_pop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) 
   const float lim = L.limit(P.cull_eps);
   while (L.sp > 0) {
     --L.sp;
-    const int2 ent = L.sp < S.KL ? S.lds[L.sp * TL_LANES] : unpack_ent(S.ovf[(size_t)(L.sp - S.KL) * S.ovs]);
+    const int2 ent = L.sp < S.KL ? S.lds[L.sp * TL_LANES] : unpack_ent(*S.ovf_at(L.sp));
     if (cull && __int_as_float(ent.y) > lim) continue;
     L.cur = ent.x;
     return true;
@@ -437,6 +452,22 @@ RTD void tl_node(const KParams& P, TraceLane& L, const TraceStack& S, bool cull)
 // Split in parts: the box tests (tl_qnode_keys, planes given), the sort + push (tl_qnode_push),
 // so the finisher can fetch the node before its triangle test (tl_dual_load) while wf_trace
 // keeps the fetch inside each branch (fewer live registers at 64 VGPRs).
+// t0 / t1 of RT:312-313 for the four children of a ray with finite 1/d: near / far planes chosen
+// per ray by the load offsets (nx..fz = near x, y, z, far x, y, z); children in pairs with packed
+// fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations, two at a time)
+RTD void tl_qnode_t01(const TraceLane& L, const float4 nx, const float4 ny, const float4 nz, const float4 fx,
+                      const float4 fy, const float4 fz, float (&t0)[4], float (&t1)[4]) {
+  const v2f ox = {L.ox, L.ox}, oy = {L.oy, L.oy}, oz = {L.oz, L.oz};
+  const v2f ix = {L.ix, L.ix}, iy = {L.iy, L.iy}, iz = {L.iz, L.iz};
+  const v2f nx01 = (v2f{nx.x, nx.y} - ox) * ix, ny01 = (v2f{ny.x, ny.y} - oy) * iy, nz01 = (v2f{nz.x, nz.y} - oz) * iz;
+  const v2f nx23 = (v2f{nx.z, nx.w} - ox) * ix, ny23 = (v2f{ny.z, ny.w} - oy) * iy, nz23 = (v2f{nz.z, nz.w} - oz) * iz;
+  const v2f fx01 = (v2f{fx.x, fx.y} - ox) * ix, fy01 = (v2f{fy.x, fy.y} - oy) * iy, fz01 = (v2f{fz.x, fz.y} - oz) * iz;
+  const v2f fx23 = (v2f{fx.z, fx.w} - ox) * ix, fy23 = (v2f{fy.z, fy.w} - oy) * iy, fz23 = (v2f{fz.z, fz.w} - oz) * iz;
+  t0[0] = max_(nx01.x, max_(ny01.x, nz01.x)); t1[0] = min_(fx01.x, min_(fy01.x, fz01.x));
+  t0[1] = max_(nx01.y, max_(ny01.y, nz01.y)); t1[1] = min_(fx01.y, min_(fy01.y, fz01.y));
+  t0[2] = max_(nx23.x, max_(ny23.x, nz23.x)); t1[2] = min_(fx23.x, min_(fy23.x, fz23.x));
+  t0[3] = max_(nx23.y, max_(ny23.y, nz23.y)); t1[3] = min_(fx23.y, min_(fy23.y, fz23.y));
+}
 // t0 / t1 of RT:312-313 for the four children; the box is hit iff t1 >= t0 && t1 > 0, which is
 // exactly hitAABB(...) > 0 (RT:315); survivors get their entry t0 as sort key
 RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4 rf, const float4 p0, const float4 p1,
@@ -448,20 +479,12 @@ RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4
     r[c] = ok ? ref : Q_EMPTY;
   };
   if (L.finite) {
-    // near / far planes chosen per ray by the load offsets (p0..p5 = near x, y, z, far x, y, z);
-    // children in pairs with packed fp32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE
-    // operations, two at a time)
-    const float4 nx = p0, ny = p1, nz = p2, fx = p3, fy = p4, fz = p5;
-    const v2f ox = {L.ox, L.ox}, oy = {L.oy, L.oy}, oz = {L.oz, L.oz};
-    const v2f ix = {L.ix, L.ix}, iy = {L.iy, L.iy}, iz = {L.iz, L.iz};
-    const v2f nx01 = (v2f{nx.x, nx.y} - ox) * ix, ny01 = (v2f{ny.x, ny.y} - oy) * iy, nz01 = (v2f{nz.x, nz.y} - oz) * iz;
-    const v2f nx23 = (v2f{nx.z, nx.w} - ox) * ix, ny23 = (v2f{ny.z, ny.w} - oy) * iy, nz23 = (v2f{nz.z, nz.w} - oz) * iz;
-    const v2f fx01 = (v2f{fx.x, fx.y} - ox) * ix, fy01 = (v2f{fy.x, fy.y} - oy) * iy, fz01 = (v2f{fz.x, fz.y} - oz) * iz;
-    const v2f fx23 = (v2f{fx.z, fx.w} - ox) * ix, fy23 = (v2f{fy.z, fy.w} - oy) * iy, fz23 = (v2f{fz.z, fz.w} - oz) * iz;
-    keep(0, max_(nx01.x, max_(ny01.x, nz01.x)), min_(fx01.x, min_(fy01.x, fz01.x)), rf.x);
-    keep(1, max_(nx01.y, max_(ny01.y, nz01.y)), min_(fx01.y, min_(fy01.y, fz01.y)), rf.y);
-    keep(2, max_(nx23.x, max_(ny23.x, nz23.x)), min_(fx23.x, min_(fy23.x, fz23.x)), rf.z);
-    keep(3, max_(nx23.y, max_(ny23.y, nz23.y)), min_(fx23.y, min_(fy23.y, fz23.y)), rf.w);
+    float t0[4], t1[4];
+    tl_qnode_t01(L, p0, p1, p2, p3, p4, p5, t0, t1);
+    keep(0, t0[0], t1[0], rf.x);
+    keep(1, t0[1], t1[1], rf.y);
+    keep(2, t0[2], t1[2], rf.z);
+    keep(3, t0[3], t1[3], rf.w);
   } else {  // a direction component is exactly 0: the literal slab (0 * inf -> NaN cases);
             // p0..p5 = lo x, y, z, hi x, y, z
     const float4 lx = p0, ly = p1, lz = p2, hx = p3, hy = p4, hz = p5;
@@ -537,6 +560,97 @@ RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   }
   return tl_qnode_push<POP>(P, L, S, cull, k, r);
 }
+// ---- fast traversal (wf_trace MODE_FAST): rays with a finite 1/d and no exact distance tie; the
+// rest are deferred to the exact kernel (MODE_SLOWIN), which traces them from scratch.
+// The kept children of a node are pushed in the node's precomputed order for the ray's direction
+// octant (QNode::ord) instead of being sorted by entry distance: every child's stack position is
+// the number of kept children that come after it (a popcount of its ord nibble against the kept
+// mask), so the four stores are unconditional (an unkept child lands on a free slot above the new
+// top) and the nearest kept child is simply the top, which the iteration's single pop takes.
+// Order only decides how soon `best` tightens: the closest hit stays exact (culling bound, ties
+// deferred), DESIGN.md §2.
+RTD void tl_store(const TraceStack& S, int idx, int2 ent) {  // the entry at stack index idx
+  if (idx < S.KL) S.lds[idx * TL_LANES] = ent;
+  else *S.ovf_at(idx) = pack_ent(ent);
+}
+RTD void tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+  const uint32_t off = (uint32_t)L.cur << 7;  // (low 7 bits zero: | adds an in-node offset)
+  const uint32_t pk = L.offPk;
+  const int4 rf = ld<int4>(P.qnodes, off + 96u);
+  const uint32_t M = ld<unsigned short>(P.qnodes, (off | (pk >> 24)) + 112u);
+  const uint32_t ax = off | (pk & 0xffu), ay = off | ((pk >> 8) & 0xffu), az = off | ((pk >> 16) & 0xffu);
+  const float4 nx = ld<float4>(P.qnodes, ax), ny = ld<float4>(P.qnodes, ay), nz = ld<float4>(P.qnodes, az);
+  const float4 fx = ld<float4>(P.qnodes, ax ^ 48u), fy = ld<float4>(P.qnodes, ay ^ 80u), fz = ld<float4>(P.qnodes, az ^ 112u);
+  float t0[4], t1[4];
+  tl_qnode_t01(L, nx, ny, nz, fx, fy, fz, t0, t1);
+  const float lim = cull ? L.limit(P.cull_eps) : __int_as_float(0x7f800000);
+  // hit (t1 >= t0 && t1 > 0, RT:315) and not culled (t0 <= lim): with the smallest positive float
+  // dmin and lim > 0, exactly max(t0, dmin) <= min(t1, lim) (an empty slot: t0 = +inf, t1 = -inf)
+  const float dmin = __int_as_float(1);
+  bool ok[4];
+  uint32_t kept = 0u;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    ok[c] = max_(t0[c], dmin) <= min_(t1[c], lim);
+    kept |= ok[c] ? (1u << c) : 0u;
+  }
+  const int n = __popc(kept);
+  const uint32_t A = M & (kept * 0x1111u);
+  const int r[4] = {rf.x, rf.y, rf.z, rf.w};
+  int f[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) f[c] = ok[c] ? __popc((A >> (4 * c)) & 15u) : n;
+  if (L.sp + 4 <= S.KL) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) S.lds[(L.sp + f[c]) * TL_LANES] = make_int2(r[c], __float_as_int(t0[c]));
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      if (ok[c]) tl_store(S, L.sp + f[c], make_int2(r[c], __float_as_int(t0[c])));
+  }
+  L.sp += n;
+}
+#ifndef RT_FAST_DEFER_EDGES  // fast traversal: a point the edge filter cannot decide defers the ray (1) or
+                             // runs the reference's edge functions in place (0)
+#define RT_FAST_DEFER_EDGES 0
+#endif
+// one triangle for the fast traversal: 0 no closer hit, 1 the new closest hit, 2 defer the ray (an
+// exact distance tie with the current best, whose order rule tie_wins lives in the exact kernel)
+RTD int tl_triangle_fast(const KParams& P, TraceLane& L, int i) {
+  const uint32_t off = (uint32_t)i * 48u;
+  const float4 A = ld<float4>(P.trx, off), B = ld<float4>(P.trx, off + 16u), Cc = ld<float4>(P.trx, off + 32u);
+  const f3 p1 = xyz(A);
+  const f3 ng = mk3(A.w, B.w, Cc.w);
+  const float dn = dot(ng, L.d());
+  const float num = dot(ng, p1) - dot(L.o(), ng);
+  const float t = num / dot(L.d(), ng);                                // RT:265
+  const float dist = t - 0.00001f;
+  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (dist <= L.best);  // RT:262, 268, 328/356
+  const f3 Pp = L.o() + L.d() * t;
+  const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
+  const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
+  const float b3 = __builtin_fmaf(Cc.x, qx, __builtin_fmaf(Cc.y, qy, Cc.z * qz));
+  const float b1 = (1.0f - b2) - b3;
+  const float mn = fminf(b1, fminf(b2, b3));
+  const float dq = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
+  const float lr = fmaxf(fabsf(B.x), fmaxf(fabsf(B.y), fabsf(B.z))) + fmaxf(fabsf(Cc.x), fmaxf(fabsf(Cc.y), fabsf(Cc.z)));
+  const float m = (dq * lr) * P.tri_k1 + P.tri_k0;
+  bool inside = mn > 0.0f;
+  const bool undecided = ok & !((fabsf(mn) > m) & (m < 0.25f));
+  if (RT_FAST_DEFER_EDGES) {
+    if (undecided) return 2;
+  } else if (undecided) {
+    inside = tl_edges_exact(P, i, p1, ng, Pp);
+  }
+  ok &= inside;
+  if (!ok) return 0;
+  if (dist == L.best) return 2;
+  L.best = dist;
+  L.besttri = i;
+  L.bestt = t;
+  return 1;
+}
+
 // the node fetch alone (the finisher issues it before its triangle test): rf + six planes, near /
 // far for a finite 1/d, lo / hi otherwise (tl_start's offsets cover both)
 struct QLoad {
@@ -573,6 +687,8 @@ RTD void tl_start(const KParams& P, TraceLane& L) {
   L.offNx = (L.ix > 0.0f || !L.finite) ? 0 : 48;
   L.offNy = (L.iy > 0.0f || !L.finite) ? 16 : 64;
   L.offNz = (L.iz > 0.0f || !L.finite) ? 32 : 80;
+  L.offPk = (uint32_t)L.offNx | (uint32_t)L.offNy << 8 | (uint32_t)L.offNz << 16 |
+            (uint32_t)(2 * ((L.ix < 0.0f ? 1 : 0) | (L.iy < 0.0f ? 2 : 0) | (L.iz < 0.0f ? 4 : 0))) << 24;
   L.best = INF;
   L.besttri = -1;
   L.bestt = 0.0f;
@@ -700,21 +816,31 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #endif
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
 // passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
-// a separate instantiation: the code alone cost the bulk's kernels 0.4%)
-template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false>  // P1: pass 1's 16-B rays
+// a separate instantiation: the code alone cost the bulk's kernels 0.4%).
+// MODE: MODE_EXACT traces every ray of the pass with the exact order rules (distance-sorted pushes,
+// tie_wins, the literal slab for a zero direction component); MODE_FAST (the 4-wide tree, no visit
+// counting) traces the rays with a finite 1/d in octant order (tl_qnode_fast) and defers a ray
+// with a zero direction component or an exact distance tie to the slow list (the pass's free
+// queue buffer, queue[qin ^ 1], count cnt[5]); MODE_SLOWIN is the exact kernel over that list
+// (claim counter cnt[6]), launched right after the fast one.
+enum { MODE_EXACT = 0, MODE_FAST = 1, MODE_SLOWIN = 2 };
+template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false, int MODE = MODE_EXACT>  // P1: pass 1's 16-B rays
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
+  static_assert(MODE == MODE_EXACT || (WIDE && !COUNT), "fast / slow-list modes: 4-wide tree, no visit counting");
+  static_assert(MODE != MODE_SLOWIN || !STATIC, "the slow list is claimed dynamically");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int qin = W.pass & 1;
-  const unsigned int nq = CAM ? W.cam_n : S.cnt[qin];
+  int* const slow_list = S.queue[qin ^ 1];  // free during this pass's traversal (the next shade fills it)
+  const unsigned int nq = MODE == MODE_SLOWIN ? S.cnt[5] : CAM ? W.cam_n : S.cnt[qin];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
     S.cnt[qin ^ 1] = 0u;
     S.cnt[2 + (qin ^ 1)] = 0u;
   }
   if (nq == 0u || !P.has_scene) {
-    if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
+    if (!P.has_scene && MODE != MODE_SLOWIN) {  // empty scene: every ray misses (RT:346 reads a zero node)
       for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
         const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
         S.res[e] = make_int2(-1, 0);
@@ -727,8 +853,9 @@ void wf_trace(const WFParams W) {
   // overflow region ([entry][grid lane], coalesced) that only very deep stacks touch.
   TraceStack TS;
   TS.KL = P.lds_entries;
-  TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
-  TS.ovf = (gu64*)(P.stack_ovf) + (blockIdx.x * TL_LANES + threadIdx.x);
+  TS.lds0 = reinterpret_cast<int2*>(smem);
+  TS.lds = TS.lds0 + threadIdx.x;
+  TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
   TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
 
@@ -782,7 +909,7 @@ void wf_trace(const WFParams W) {
       if (pool_next >= pool_end) {
         const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
+        if (lane == 0) base = atomicAdd(&S.cnt[MODE == MODE_SLOWIN ? 6 : 4], chunk);
         base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= nq) {
           drained = true;
@@ -793,10 +920,12 @@ void wf_trace(const WFParams W) {
       }
       if (!drained || pool_next < pool_end) {
         const unsigned int avail = pool_end - pool_next;
-        const unsigned int rank = (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
+        // idle lanes below this one (v_mbcnt: no per-lane 64-bit mask kept across the loop)
+        const unsigned int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         if (!busy && rank < avail) {
-          const unsigned int slot = pool_next + rank;
+          const unsigned int qi = pool_next + rank;
           if (CAM) {  // implicit camera pass: queue entry i is slot i's camera ray
+            const unsigned int slot = MODE == MODE_SLOWIN ? (unsigned int)slow_list[qi] >> 1 : qi;
             entry = (int)(slot << 1);
             L.anyhit = false;
             uint32_t seed_unused, frame_unused;
@@ -804,7 +933,7 @@ void wf_trace(const WFParams W) {
             L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
             L.dx = d.x; L.dy = d.y; L.dz = d.z;
           } else {
-            entry = S.queue[qin][slot];
+            entry = MODE == MODE_SLOWIN ? slow_list[qi] : S.queue[qin][qi];
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
             const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
@@ -819,6 +948,10 @@ void wf_trace(const WFParams W) {
           }
           tl_start<WIDE>(P, L);
           busy = true;
+          if (MODE == MODE_FAST && !L.finite) {  // a zero direction component: the literal slab (exact kernel)
+            slow_list[atomicAdd(&S.cnt[5], 1u)] = entry;
+            busy = false;
+          }
         }
         pool_next += min((unsigned int)__popcll(idle), avail);
       }
@@ -826,8 +959,36 @@ void wf_trace(const WFParams W) {
     if (!__any(busy)) break;
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
+    bool defer = false;  // MODE_FAST: the ray goes to the slow list
     if (COUNT) { v_itN++; v_itT++; }
-    if (busy) {
+    if (MODE == MODE_FAST && busy) {
+      // one triangle of the current leaf and one node step, then the iteration's single pop: a
+      // taken leaf, or the node's nearest kept child (the top of the stack after the pushes)
+      if (L.tri_i < L.tri_end) {
+        const int h = tl_triangle_fast(P, L, L.tri_i++);
+        if (h == 2) {
+          finished = defer = true;
+        } else if (h == 1 && L.anyhit) {
+          finished = true;
+          L.tri_end = L.tri_i;
+        }
+      }
+      bool needPop = false;
+      if (!finished && L.haveCur) {
+        if (ref_is_leaf(L.cur)) {
+          if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
+            L.tri_i = leaf_first(L.cur);
+            L.tri_end = L.tri_i + leaf_count(L.cur);
+            needPop = true;
+          }
+        } else {
+          tl_qnode_fast(P, L, TS, cull);
+          needPop = true;
+        }
+      }
+      if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
+      if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
+    } else if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
         if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
@@ -860,6 +1021,10 @@ void wf_trace(const WFParams W) {
       }
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
+    }
+    if (MODE == MODE_FAST && busy && defer) {
+      slow_list[atomicAdd(&S.cnt[5], 1u)] = entry;
+      busy = false;
     }
     if (busy && finished) {
       S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
@@ -1296,7 +1461,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.cnt[4] = 0u;  // fetch counter of the next trace pass
-    if (na) atomicAdd(&P.stats[16], (unsigned long long)na);  // path shade steps (rt_stats.path_steps)
+    S.cnt[5] = 0u;  // its slow list (MODE_FAST -> MODE_SLOWIN) and that list's claim counter
+    S.cnt[6] = 0u;
+    if (na) {
+      atomicAdd(&P.stats[16], (unsigned long long)na);  // path shade steps (rt_stats.path_steps)
+      if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
+    }
   }
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
@@ -1433,8 +1603,9 @@ void wf_finish(const WFParams W) {
 #endif
   TraceStack TS;
   TS.KL = P.lds_entries;
-  TS.lds = reinterpret_cast<int2*>(smem) + threadIdx.x;
-  TS.ovf = (gu64*)(P.stack_ovf) + (blockIdx.x * TL_LANES + threadIdx.x);
+  TS.lds0 = reinterpret_cast<int2*>(smem);
+  TS.lds = TS.lds0 + threadIdx.x;
+  TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
   TS.ovs = P.ovf_lanes;
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
   unsigned long long nrays = 0, nsamples = 0, nsteps = 0;
@@ -1576,7 +1747,7 @@ void wf_finish(const WFParams W) {
   if (lane == 0) {
     atomicAdd(&P.stats[0], nrays);
     atomicAdd(&P.stats[1], nsamples);
-    atomicAdd(&P.stats[16], nsteps);
+    atomicAdd(&P.stats[20], nsteps);  // rt_stats.finish_steps
   }
 }
 

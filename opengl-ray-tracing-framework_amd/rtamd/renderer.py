@@ -24,6 +24,8 @@ RT_FLAG_COUNT_VISITS = 2
 RT_FLAG_MEGAKERNEL = 4
 RT_FLAG_NO_FINISH = 8
 RT_FLAG_FINISH = 16
+RT_FLAG_SERIAL = 32
+RT_ABI_VERSION = 4
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 
 _f32p = C.POINTER(C.c_float)
@@ -37,7 +39,7 @@ ABI_SYMBOLS = (
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
     "rt_tile_costs", "rt_set_finish", "rt_order_work", "rt_set_pipeline",
-    "rt_tonemap_async", "rt_display_fetch",
+    "rt_tonemap_async", "rt_display_fetch", "rt_stats_get_sized", "rt_abi_version",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -81,7 +83,10 @@ class RtStats(C.Structure):
                 ("leaf_pops", C.c_uint64), ("tri_tests", C.c_uint64), ("launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("trace_launches", C.c_uint64), ("trace_ms", C.c_double),
                 ("trace_iters", C.c_uint64), ("trace_iters_max", C.c_uint64), ("path_steps", C.c_uint64),
-                ("p1_rays", C.c_uint64)]
+                ("p1_rays", C.c_uint64),
+                # ABI 4
+                ("pass0_steps", C.c_uint64), ("pass1_steps", C.c_uint64), ("finish_steps", C.c_uint64),
+                ("trace_busy_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -177,6 +182,9 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_render.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(RtStats)]
     L.rt_synchronize.argtypes = [vp]
     L.rt_stats_get.argtypes = [vp, C.POINTER(RtStats)]
+    if hasattr(L, "rt_stats_get_sized"):  # ABI >= 4 (older builds are loaded for A/B timing)
+        L.rt_stats_get_sized.argtypes = [vp, C.POINTER(RtStats), C.c_size_t]
+        L.rt_abi_version.argtypes = []
     L.rt_stats_reset.argtypes = [vp]
     L.rt_get_stream.argtypes = [vp, C.POINTER(vp)]
     L.rt_set_stream.argtypes = [vp, vp]
@@ -370,8 +378,11 @@ class Renderer:
         self._check(self._L.rt_synchronize(self._h), "rt_synchronize")
 
     def stats(self) -> dict:
-        st = RtStats()
-        self._check(self._L.rt_stats_get(self._h, C.byref(st)), "rt_stats_get")
+        st = RtStats()  # zero-filled: a pre-ABI-4 build leaves the newer fields 0
+        if hasattr(self._L, "rt_stats_get_sized"):
+            self._check(self._L.rt_stats_get_sized(self._h, C.byref(st), C.sizeof(st)), "rt_stats_get_sized")
+        else:
+            self._check(self._L.rt_stats_get(self._h, C.byref(st)), "rt_stats_get")
         return st.as_dict()
 
     def reset_stats(self) -> None:

@@ -52,3 +52,23 @@ def test_release_library_reads_no_environment():
     assert b"getenv" not in rel
     assert b"RT_CULL_EPS_SCALE" not in rel and b"RT_BVH_WIDTH" not in rel
     assert b"RT_CULL_EPS_SCALE" in dev and b"getenv" in dev
+
+
+def test_stats_struct_matches_header(tmp_path):
+    """The ctypes rt_stats mirrors include/rt_abi.h field for field (offsets and size from gcc on the
+    header itself), and rt_abi_version() (no device needed) is the header's RT_ABI_VERSION."""
+    fields = [f for f, _ in renderer.RtStats._fields_]
+    src = tmp_path / "probe.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt_abi.h"\nint main(void) {\n'
+                   '  printf("%zu %d\\n", sizeof(rt_stats), RT_ABI_VERSION);\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(rt_stats, {f}));\n' for f in fields) + "  return 0;\n}\n")
+    import subprocess
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    size, ver = int(out[0]), int(out[1])
+    assert size == C.sizeof(renderer.RtStats)
+    assert [int(x) for x in out[2:]] == [getattr(renderer.RtStats, f).offset for f in fields]
+    assert ver == renderer.RT_ABI_VERSION
+    lib = C.CDLL(str(ROOT / "opengl-ray-tracing-framework_amd" / "lib" / "librtamd.so"))
+    assert lib.rt_abi_version() == ver

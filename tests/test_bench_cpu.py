@@ -70,6 +70,8 @@ def test_bench_self_launches_two_gloo_ranks():
     d = _bench("--gpus", "2", "--steps", "20", "--warmup", "5", "--dry-run")
     assert d["n_gpus"] == 2 and d["gather_ok"]
     assert d["pixels_covered"] == 1920 * 1080
+    co = d["collective"]
+    assert co["backend"] == "gloo" and co["world"] == 2 and len(co["rank_ms"]) == 2
 
 
 def test_bench_launcher_stops_the_other_ranks_when_one_fails():
@@ -97,30 +99,79 @@ def test_trace_ray_bytes_follow_the_path_state_layout():
     assert bench.B_RAY_CAMERA == 8
 
 
-def test_roofline_names_its_limiter_at_the_spec_clock():
-    """The roofline block prices wf_trace against HBM (the contract's roofline) and names the
-    limiter from the measured utilisations; VALU issue is computed at the 2.4 GHz spec clock over
-    the standalone launch time, so no field implies a clock or a bandwidth above the hardware's."""
+def test_roofline_bound_follows_the_limiter():
+    """The roofline block prices wf_trace at its STANDALONE launch time (the probe render, one frame
+    group), names the limiter from the utilisations (HBM, VALU issue at the 2.4 GHz spec clock, L2)
+    and reports achieved / peak / frac of that bound, the HBM roofline beside it (VERDICT r3 weak
+    #4).  No field implies a clock, a bandwidth or a kernel time per step above what was measured."""
     import bench
-    st = {"rays": 2_000_000_000, "samples": 800_000_000, "trace_launches": 10, "path_steps": 1_000_000_000}
+    st = {"rays": 2_000_000_000, "samples": 800_000_000, "trace_launches": 10, "trace_ms": 160.0,
+          "path_steps": 1_000_000_000, "pass0_steps": 200_000_000, "pass1_steps": 300_000_000}
+    probe = {"rays": 1_000_000_000, "samples": 400_000_000, "trace_launches": 5, "trace_ms": 60.0, "frames": 7}
     vis = {"rays": 1000, "internal_pops": 3000, "tri_tests": 3000}
     prof = {"_file": "profiles/x.json", "kernels": {
         "wf_trace": {"avg_launch_ms": 16.0, "avg_launch_ms_standalone": 12.0, "hbm_bytes_per_launch": 1.2e10,
-                     "SQ": {"SQ_INSTS_VALU": 6.6e9, "SQ_ACTIVE_INST_VALU": 6.7e9, "SQ_THREAD_CYCLES_VALU": 1.9e11}},
+                     "SQ": {"SQ_INSTS_VALU": 6.6e9, "SQ_INSTS_SALU": 3.3e9, "SQ_ACTIVE_INST_VALU": 6.7e9,
+                            "SQ_THREAD_CYCLES_VALU": 1.9e11}},
         "wf_shade": {"avg_launch_ms": 13.0, "avg_launch_ms_standalone": 6.0, "hbm_bytes_per_launch": 3.0e10}}}
-    r = bench.roofline(st, vis, None, prof, 16.0)
-    assert r["bound"] == "hbm" and r["kernel"] == "wf_trace"
-    r1 = bench.roofline(dict(st, p1_rays=500_000_000), vis, None, prof, 16.0)
-    assert r["algorithmic_bytes_per_launch"] - r1["algorithmic_bytes_per_launch"] == 50_000_000 * 8
-    assert r["valu"]["spec_clock_ghz"] == 2.4
+    r = bench.roofline(st, vis, None, prof, probe, 2)
+    assert r["kernel"] == "wf_trace" and r["avg_launch_ms"] == 12.0 and "standalone" in r["avg_launch_ms_regime"]
+    # algorithmic bytes of the probe's launches: 8 B per camera ray, 36 B per other secondary ray
+    assert r["hbm"]["algorithmic_bytes_per_launch"] == round((8 * 400e6 + 36 * 600e6) / 5)
+    r1 = bench.roofline(st, vis, None, prof, dict(probe, p1_rays=50_000_000), 2)
+    assert r["hbm"]["algorithmic_bytes_per_launch"] - r1["hbm"]["algorithmic_bytes_per_launch"] == 10_000_000 * 8
     want = 6.6e9 * 2 / (1024 * 2.4e9 * 12e-3)
-    assert abs(r["valu"]["issue_frac_at_spec_clock"] - want) < 1e-4
+    assert abs(r["valu"]["frac"] - want) < 1e-4 and r["valu"]["spec_clock_ghz"] == 2.4
+    assert r["valu"]["salu_per_valu"] == 0.5
     assert r["limiter"] == max(r["utilisation"], key=r["utilisation"].get) == "valu_issue"
+    assert r["bound"] == "valu_issue" and r["frac"] == r["valu"]["frac"] and r["unit"] == r["valu"]["unit"]
     assert all(0 < v < 1 for v in r["utilisation"].values())
     sh = r["kernels"]["wf_shade"]
     assert sh["path_steps_per_launch"] == 100_000_000
+    assert sh["algorithmic_bytes_per_launch"] == round((92 * 200e6 + 176 * 300e6 + 184 * 500e6) / 10)
     assert 0 < sh["frac"] < sh["traffic_frac"] < 1
-    assert "clock_ghz" not in r["valu"]
+    # per-step kernel time implied by each per-launch figure stays within the step
+    assert r["avg_launch_ms"] * r["launches_per_step"] <= st["trace_ms"] / 2 * 1.0001
+    # no probe: the co-running time, labelled as such
+    r2 = bench.roofline(st, None, None, None, None, 2)
+    assert r2["avg_launch_ms"] == 16.0 and "co-running" in r2["avg_launch_ms_regime"] and r2["bound"] == "hbm"
+
+
+def _committed_bench_line():
+    """the newest committed bench line in the round-4 roofline format, and its profile"""
+    for p in sorted((ROOT / "profiles").glob("r*_bench_C3.json"), reverse=True):
+        d = json.loads(p.read_text())
+        if "avg_launch_ms_regime" in d.get("roofline", {}):
+            return p, d
+    return None, None
+
+
+def test_committed_roofline_recomputes_from_the_profile():
+    """every roofline figure of the committed bench line is recomputable from
+    profiles/ and consistent with the step: frac = algorithmic bytes (or VALU instructions) per
+    launch / the standalone launch time; the standalone time agrees with rocprof's standalone
+    launches within 5%; wf_trace and wf_shade per-launch times x launches per step fit in the step;
+    bound = limiter."""
+    p, d = _committed_bench_line()
+    if p is None:
+        pytest.skip("no committed round-4 bench line yet")
+    rf = d["roofline"]
+    prof = json.loads((ROOT / rf["profile"]).read_text())
+    kt = prof["kernels"]["wf_trace"]
+    t = rf["avg_launch_ms"]
+    assert abs(rf["hbm"]["achieved"] - rf["hbm"]["algorithmic_bytes_per_launch"] / (t * 1e-3) / 1e9) < 0.2
+    assert abs(rf["hbm"]["frac"] - rf["hbm"]["achieved"] / 8000.0) < 1e-4
+    v = rf["valu"]
+    assert abs(v["achieved"] - kt["SQ"]["SQ_INSTS_VALU"] / (t * 1e-3) / 1e9) < 0.2
+    assert abs(v["frac"] - v["achieved"] / (1024 * 2.4 / 2)) < 1e-4
+    assert rf["bound"] == rf["limiter"] == max(rf["utilisation"], key=rf["utilisation"].get)
+    std = kt.get("probe_avg_launch_ms") or kt["avg_launch_ms_standalone"]
+    assert abs(std / t - 1) < 0.05, (std, t)
+    assert t * rf["launches_per_step"] <= d["ms_per_step"]
+    sh = rf["kernels"]["wf_shade"]
+    assert sh["avg_launch_ms_standalone"] * sh["launches_per_step"] <= d["ms_per_step"]
+    assert abs(sh["frac"] - sh["algorithmic_bytes_per_launch"] / (sh["avg_launch_ms_standalone"] * 1e-3) / 8e12) < 1e-3
+    assert d["kernel"]["busy_ms_per_step"] <= d["ms_per_step"]
 
 
 def test_cpu_baseline_records_the_host():

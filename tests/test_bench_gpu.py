@@ -30,6 +30,12 @@ def test_multi_rank_bench_frame_equals_one_rank(n, extra):
     assert many["n_gpus"] == n and many["rehearsal"]
     assert many["frame_sha256"] == one["frame_sha256"]
     assert many["rays_per_sample"] == one["rays_per_sample"]
+    # the line shows which collective backend saw how many ranks, and each rank's time
+    co = many["collective"]
+    assert co["backend"] == "gloo" and co["world"] == n and co["rehearsal"]
+    assert len(co["rank_ms"]) == n and len(co["gather_ms_per_rank"]) == n and co["gather_ms"] >= 0
+    assert co["rank_max_over_mean"] >= 1.0
+    assert one["collective"]["world"] == 1 and one["collective"]["backend"] is None
 
 
 def test_eight_rank_bench_at_full_size_frame_equals_one_rank():

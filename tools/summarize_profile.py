@@ -14,8 +14,11 @@ Standalone duration = the mean launch duration in the PMC passes' own kernel tra
 collection serialises the dispatches); the trace pass's durations are the co-running ones.
 Effective clock = GRBM_GUI_ACTIVE / 8 (summed over the XCDs) / the same pass's standalone
 duration (same guide, DVFS), reported only for launches of >= 0.3 ms (shorter ones read high).
-Counters are taken from the timed bench launches (wf_*<false, ...>; the visit-counting frame
-runs the <true, ...> instantiation and is excluded).
+Launches are taken from the bench run up to its visit-counting frame: every dispatch from the first
+wf_trace<true, ...> (the COUNT instantiation that frame runs) on is dropped, wf_shade's included
+(its 18 near-empty launches had been averaged in).  probe_avg_launch_ms = the mean of the
+last `probe_trace_launches` wf_trace launches before that frame in the trace pass: bench.py's
+standalone probe (one frame group, RT_FLAG_SERIAL), the figure its roofline divides by.
 """
 import csv
 import json
@@ -40,9 +43,16 @@ def kname(full):
     return None
 
 
+def rows(path):
+    """kernel-trace / counter rows of one pass, in dispatch order, up to the visit-count frame"""
+    rs = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
+    cut = next((int(r["Dispatch_Id"]) for r in rs if "wf_trace<true" in r["Kernel_Name"]), None)
+    return [r for r in rs if cut is None or int(r["Dispatch_Id"]) < cut]
+
+
 shutil.copyfile(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
 durs, regs = defaultdict(list), {}
-for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")):
+for r in rows(src / "trace" / "run_kernel_trace.csv"):
     k = kname(r["Kernel_Name"])
     if k:
         durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
@@ -56,7 +66,7 @@ def standalone(name):
     p = src / name / "run_kernel_trace.csv"
     out = defaultdict(dict)
     if p.exists():
-        for r in csv.DictReader(open(p)):
+        for r in rows(p):
             k = kname(r["Kernel_Name"])
             if k:
                 out[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
@@ -69,7 +79,7 @@ def counters(name):
     p = src / name / "run_counter_collection.csv"
     if not p.exists():
         return {}
-    for r in csv.DictReader(open(p)):
+    for r in rows(p):
         k = kname(r["Kernel_Name"])
         if k:
             out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -108,6 +118,10 @@ for k in KERNELS:
         e["wave_cycle_split"] = {"waiting": round(c.get("SQ_WAIT_ANY", 0) / w, 3),
                                  "issue_stalled": round(c.get("SQ_WAIT_INST_ANY", 0) / w, 3),
                                  "issuing": round(c.get("SQ_ACTIVE_INST_ANY", 0) / w, 3)}
+    npr = int(cfg.get("probe_trace_launches", 0))
+    if k == "wf_trace" and npr and len(durs[k]) > npr:
+        e["probe_avg_launch_ms"] = round(statistics.mean(durs[k][-npr:]), 4)
+        e["probe_launches"] = npr
     if c.get("TCC_HIT_sum"):
         e["l2_hit"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
     summary["kernels"][k] = e
@@ -122,6 +136,7 @@ if cfg.get("config") and "wf_trace" in summary["kernels"]:
         if t:
             pm["kernels"][k] = {
                 "avg_launch_ms": t["avg_launch_ms"], "avg_launch_ms_standalone": t.get("avg_launch_ms_standalone"),
+                "probe_avg_launch_ms": t.get("probe_avg_launch_ms"),
                 "hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"), "effective_clock_ghz": t.get("effective_clock_ghz"),
                 "wave_cycle_split": t.get("wave_cycle_split"),
                 "SQ": {n: v for n, v in t["counters_per_launch"].items() if n.startswith("SQ_")}}
