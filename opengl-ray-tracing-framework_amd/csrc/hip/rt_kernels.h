@@ -46,6 +46,7 @@ struct KParams {
   int root, has_scene, stack_entries;
   const QNode* __restrict__ qnodes;  // 4-wide collapse of `nodes` (wavefront trace, TW_WIDE)
   int qroot;
+  int n_qnodes, n_tri;              // (bounds of the RT_CHECK development build)
   int lds_entries;                  // wavefront traversal: stack entries kept in LDS
   float cull_eps;                   // culling bound: accepted hit points lie within this of their box
   int pool_chunk;                   // wavefront traversal: rays claimed per queue atomic

@@ -33,7 +33,7 @@ struct rt_ctx {
   // scene
   GNode* d_nodes = nullptr;
   rtd::QNode* d_qnodes = nullptr;
-  int qroot = 0, qstack_entries = 2;
+  int qroot = 0, qstack_entries = 2, n_qnodes = 0;
   bool wide = false;                          // 4-wide traversal available for this scene
   float4* d_tri = nullptr;
   float4* d_trx = nullptr;  // traversal records (tri_filter.h)
@@ -95,7 +95,10 @@ struct rt_ctx {
   };
   FrameTable ft[5];
   int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
-  bool fast_trace = false;                    // wf_trace MODE_FAST + MODE_SLOWIN (dev: RT_FAST_TRACE=0, the exact kernel alone)
+#ifndef RT_FAST_TRACE_DEFAULT
+#define RT_FAST_TRACE_DEFAULT 0
+#endif
+  bool fast_trace = RT_FAST_TRACE_DEFAULT;    // wf_trace MODE_FAST + MODE_SLOWIN (dev: RT_FAST_TRACE=0/1)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
@@ -136,6 +139,12 @@ struct rt_ctx {
   int finish_pass = 2;  // C3 1080p single frames: 1 / 2 / 3 -> 3.73 / 3.35 / 3.41 ms (off: 3.79)
   uint64_t finish_slots = uint64_t(8) << 20;
   int finish_bpc = 0;              // wf_finish blocks per CU
+  // wf_finish path compaction: rounds (launches) and the busy-lane count below which a drained
+  // wave hands its paths to the next round (rtd::wf_finish); 1 round = none
+#ifndef RT_FINISH_ROUNDS_DEFAULT
+#define RT_FINISH_ROUNDS_DEFAULT 1
+#endif
+  int finish_rounds = RT_FINISH_ROUNDS_DEFAULT, finish_handoff = 16;
   // Pipelined one-frame calls (rt_set_pipeline, depth D = 2): one-frame call k runs as a single
   // group on stream aux[1 + p], p = k mod D, with path-state set wfg[p], camera table p and frame
   // table ft[1 + p], so call k+1's early passes fill the CUs that call k's latency-bound finisher
@@ -508,9 +517,10 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     }
     int refs[4] = {rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY, rtd::Q_EMPTY};
     for (size_t i = 0; i < sl.size(); i++) refs[i] = is_leaf(sl[i].ref) ? sl[i].ref : build(sl[i].ref, depth + 1);
-    // an empty slot is the inverted box lo = +inf, hi = -inf: for every finite 1/d its entry t0 is
-    // +inf and its exit t1 -inf (and for a zero component the literal slab leaves the other axes
-    // deciding), so no slab test ever hits it
+    // an empty slot is the inverted box lo = +inf, hi = -inf: for a finite 1/d the sign-selected
+    // planes give entry t0 = +inf and exit t1 = -inf, so the slab test never hits it (the literal
+    // slab of a ray with a zero direction component tests the slot's ref instead: its per-axis
+    // min / max would turn the inverted box into an infinite one)
     const float pinf = INFINITY;
     float lo[3][4], hi[3][4];
     for (int k = 0; k < 3; k++)
@@ -521,6 +531,8 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     // fast traversal's child order per ray-direction octant o (bit a set: component a of the
     // direction negative): children by the projection of their box centre onto the octant's
     // diagonal, nearest first; ord[o] holds, in nibble c, the children that come after child c
+    // (dev RT_ORD_KEY=corner: by the box corner a ray of the octant enters first instead)
+    static const bool ord_corner = knob("RT_ORD_KEY") && strcmp(knob("RT_ORD_KEY"), "corner") == 0;
     uint16_t ord[8];
     for (int o = 0; o < 8; o++) {
       double key[4];
@@ -528,8 +540,11 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
         key[i] = HUGE_VAL;
         if (i < (int)sl.size()) {
           key[i] = 0.0;
-          for (int k = 0; k < 3; k++)
-            key[i] += (((o >> k) & 1) ? -0.5 : 0.5) * ((double)sl[i].lo[k] + (double)sl[i].hi[k]);
+          for (int k = 0; k < 3; k++) {
+            const bool neg = ((o >> k) & 1) != 0;
+            if (ord_corner) key[i] += neg ? -(double)sl[i].hi[k] : (double)sl[i].lo[k];
+            else key[i] += (neg ? -0.5 : 0.5) * ((double)sl[i].lo[k] + (double)sl[i].hi[k]);
+          }
         }
       }
       uint32_t m = 0;
@@ -838,6 +853,8 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
   if (const char* e = knob("RT_FAST_TRACE")) c->fast_trace = atoi(e) != 0;
+  if (const char* e = knob("RT_FINISH_ROUNDS")) c->finish_rounds = std::max(1, std::min(4, atoi(e)));
+  if (const char* e = knob("RT_FINISH_HANDOFF")) c->finish_handoff = std::max(0, std::min(64, atoi(e)));
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess || hipEventCreate(&c->t_ref) != hipSuccess ||
       hipEventRecord(c->t_ref, c->stream) != hipSuccess) {
@@ -1002,6 +1019,7 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
   if (qn.empty()) qn.push_back(rtd::QNode{});
   int rc;
   if ((rc = upload(c, (void**)&c->d_qnodes, qn.data(), qn.size() * sizeof(rtd::QNode)))) return rc;
+  c->n_qnodes = (int)qn.size();
   if ((rc = upload(c, (void**)&c->d_nodes, gn.data(), gn.size() * sizeof(GNode)))) return rc;
   if ((rc = upload(c, (void**)&c->d_tri, tri.data(), tri.size() * sizeof(float4)))) return rc;
   {  // traversal records: {p1, Ng.x} {R2, Ng.y} {R3, Ng.z} and the edge filter's margin
@@ -1454,7 +1472,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.cost_blocks = c->cost_blocks ? 1 : 0;
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
-    P.qnodes = c->d_qnodes; P.qroot = c->qroot;
+    P.qnodes = c->d_qnodes; P.qroot = c->qroot; P.n_qnodes = c->n_qnodes; P.n_tri = c->n_tri;
     {  // eps of the culling bound for this call's origins (camera position, scene points)
       double R = c->cull_R;
       for (int a = 0; a < 3; a++) R = std::max(R, std::fabs((double)fp->position[a]));
@@ -1560,6 +1578,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
+        WP.fin_round = 0;
+        WP.fin_handoff = 0;
         // (not for frame groups of one frame each: their blends must run in frame order)
         WP.fuse_blend = (!pipe && WP.n_frames == 1 && (pix_split || G == 1) && !count) ? 1 : 0;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
@@ -1617,14 +1637,21 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               HIPCHK(c, hipEventRecord(ft0, sg[g]));
             }
 #endif
-            if (fp->enable_bsdf) {
-              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
-              else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
-            } else {
-              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<false, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
-              else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+            // rounds: waves that thin out hand their paths to the next round's full waves
+            const int rounds = std::max(1, std::min(4, c->finish_rounds));
+            for (int rnd = 0; rnd < rounds; rnd++) {
+              rtd::WFParams WR = WP;
+              WR.fin_round = rnd;
+              WR.fin_handoff = rnd + 1 < rounds ? c->finish_handoff : 0;
+              if (fp->enable_bsdf) {
+                if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
+                else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
+              } else {
+                if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<false, true>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
+                else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
+              }
+              HIPCHK(c, hipGetLastError());
             }
-            HIPCHK(c, hipGetLastError());
 #ifdef RT_DEV
             if (debug_passes) {  // development aid: the finisher's waves (syncs!)
               HIPCHK(c, hipEventRecord(ft1, sg[g]));

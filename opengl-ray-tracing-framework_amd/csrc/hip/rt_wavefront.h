@@ -27,6 +27,19 @@
 
 namespace rtd {
 
+// RT_CHECK (development build: make variant HIPEXTRA=-DRT_CHECK): bounds checks that report the
+// first bad index of a launch with printf and replace it with a harmless one instead of faulting
+#ifdef RT_CHECK
+#define RT_CHK(cond, fmt, ...)                                                     \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      printf("[rt check] %s:%d " fmt "\n", __FILE__, __LINE__, ##__VA_ARGS__);   \
+    }                                                                              \
+  } while (0)
+#else
+#define RT_CHK(cond, fmt, ...) do { } while (0)
+#endif
+
 // per-path flags (< 256: packed with the bounce in s5.y)
 enum : uint32_t {
   PF_SHADOW = 1u,      // a shadow ray was traced for the current bounce (c_nee pending)
@@ -95,6 +108,10 @@ struct WFParams {
   // per group): a finishing path blends into the accumulation itself (wf_blend's operations,
   // RT:1552) instead of writing fin for a wf_blend launch after the last pass
   int fuse_blend;
+  // wf_finish rounds (path compaction): round fin_round of a finisher that runs as several launches;
+  // a round hands a path over to the next round (instead of starting its next bounce) once its
+  // wave has drained the round's list and holds fewer than fin_handoff paths (0: never)
+  int fin_round, fin_handoff;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -309,7 +326,12 @@ struct TraceStack {
   }
   // the overflow slot of entry j (the lane from the LDS column: no 64-bit per-lane pointer lives
   // across the traversal loop)
-  RTD gu64* ovf_at(int j) const { return ovf + (size_t)(j - KL) * ovs + lane(); }
+  RTD gu64* ovf_at(int j) const {
+#ifdef RT_CHECK
+    if (j < KL || j >= KL + 64) printf("[rt check] overflow stack index %d (KL %d)\n", j, KL);
+#endif
+    return ovf + (size_t)(j - KL) * ovs + lane();
+  }
   // the lane's current queue entry, kept in LDS after the stack (one VGPR less across the loop)
   RTD int* entry_slot() const { return reinterpret_cast<int*>(lds0 + KL * TL_LANES) + lane(); }
 };
@@ -488,11 +510,14 @@ RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4
   } else {  // a direction component is exactly 0: the literal slab (0 * inf -> NaN cases);
             // p0..p5 = lo x, y, z, hi x, y, z
     const float4 lx = p0, ly = p1, lz = p2, hx = p3, hy = p4, hz = p5;
+    // (the per-axis min / max of the literal slab would make an empty slot's inverted box look
+    // infinite, so an empty slot is a miss by its ref)
     auto generic = [&](int c, float ax, float ay, float az, float bx, float by, float bz, int ref) {
       const f3 f = (mk3(bx, by, bz) - L.o()) * L.inv();
       const f3 n = (mk3(ax, ay, az) - L.o()) * L.inv();
-      keep(c, max_(min_(f.x, n.x), max_(min_(f.y, n.y), min_(f.z, n.z))),
-           min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z))), ref);
+      const bool empty = ref == Q_EMPTY;
+      keep(c, empty ? __int_as_float(0x7f800000) : max_(min_(f.x, n.x), max_(min_(f.y, n.y), min_(f.z, n.z))),
+           empty ? __int_as_float(0xff800000) : min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z))), ref);
     };
     generic(0, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, rf.x);
     generic(1, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, rf.y);
@@ -542,6 +567,12 @@ RTD bool tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool
 }
 template <bool POP = true>
 RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+#ifdef RT_CHECK
+  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) {
+    printf("[rt check] node %d of %d (sp %d)\n", L.cur, P.n_qnodes, L.sp);
+    L.cur = 0;
+  }
+#endif
   const uint32_t off = (uint32_t)L.cur << 7;
   const int4 rf = ld<int4>(P.qnodes, off + 96u);
   float k[4];
@@ -574,6 +605,12 @@ RTD void tl_store(const TraceStack& S, int idx, int2 ent) {  // the entry at sta
   else *S.ovf_at(idx) = pack_ent(ent);
 }
 RTD void tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+#ifdef RT_CHECK
+  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) {
+    printf("[rt check] fast node %d of %d (sp %d)\n", L.cur, P.n_qnodes, L.sp);
+    L.cur = 0;
+  }
+#endif
   const uint32_t off = (uint32_t)L.cur << 7;  // (low 7 bits zero: | adds an in-node offset)
   const uint32_t pk = L.offPk;
   const int4 rf = ld<int4>(P.qnodes, off + 96u);
@@ -617,6 +654,12 @@ RTD void tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool
 // one triangle for the fast traversal: 0 no closer hit, 1 the new closest hit, 2 defer the ray (an
 // exact distance tie with the current best, whose order rule tie_wins lives in the exact kernel)
 RTD int tl_triangle_fast(const KParams& P, TraceLane& L, int i) {
+#ifdef RT_CHECK
+  if ((unsigned)i >= (unsigned)P.n_tri) {
+    printf("[rt check] fast triangle %d of %d\n", i, P.n_tri);
+    i = 0;
+  }
+#endif
   const uint32_t off = (uint32_t)i * 48u;
   const float4 A = ld<float4>(P.trx, off), B = ld<float4>(P.trx, off + 16u), Cc = ld<float4>(P.trx, off + 32u);
   const f3 p1 = xyz(A);
@@ -956,7 +999,9 @@ void wf_trace(const WFParams W) {
         pool_next += min((unsigned int)__popcll(idle), avail);
       }
     }
-    if (!__any(busy)) break;
+    // (MODE_FAST: every ray the refill handed out may have been deferred, and the pool goes on:
+    // the iteration then does nothing and the next one refills)
+    if (!__any(busy) && (MODE != MODE_FAST || drained)) break;
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
     bool defer = false;  // MODE_FAST: the ray goes to the slow list
@@ -979,6 +1024,12 @@ void wf_trace(const WFParams W) {
           if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
             L.tri_i = leaf_first(L.cur);
             L.tri_end = L.tri_i + leaf_count(L.cur);
+#ifdef RT_CHECK
+            if (L.tri_end > P.n_tri) {
+              printf("[rt check] leaf ref %x: triangles %d..%d of %d\n", L.cur, L.tri_i, L.tri_end, P.n_tri);
+              L.tri_i = L.tri_end = 0;
+            }
+#endif
             needPop = true;
           }
         } else {
@@ -1198,7 +1249,13 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       const float4 oo = oo0, dd = dd0;
       const f3 ro = xyz(oo), rd = xyz(dd);
       if (r.x >= 0) {
-        const int tri = r.x;
+        int tri = r.x;
+#ifdef RT_CHECK
+        if (tri >= P.n_tri) {
+          printf("[rt check] shade: path %d pass %d result triangle %d of %d (t bits %x)\n", path, W.pass, tri, P.n_tri, r.y);
+          tri = 0;
+        }
+#endif
         const float t = __int_as_float(r.y);
         const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
         const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
@@ -1587,6 +1644,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
 #define RT_FINISH_WPE 2
 #endif
+// Path compaction (rounds): once the list is drained, waves thin out to their few long bounce chains
+// (<= 16 busy lanes for about half of the finisher's wave time, 0.11 VALU lane utilisation).  So
+// the finisher runs as rounds: in every round but the last, a wave that has drained the round's
+// list and holds fewer than fin_handoff paths writes each path whose shade step just queued its
+// next rays to the next round's list (the path's state and rays are in memory at that point, as
+// for a path of the active list) instead of tracing them, and ends when its lanes are idle; the
+// next round starts those paths on full waves.  Round r reads list r and writes list r + 1:
+// active[in ^ (r & 1)], counts cnt[2 + in] (r = 0) and cnt[11 + r - 1], claims cnt[4] (r = 0) and
+// cnt[7 + r].
 template <bool BSDF, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FINISH_WPE)))
 void wf_finish(const WFParams W) {
@@ -1594,7 +1660,12 @@ void wf_finish(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1;
-  const unsigned int na = S.cnt[2 + in];
+  const int rnd = W.fin_round;
+  const int* const list = S.active[in ^ (rnd & 1)];
+  int* const next_list = S.active[in ^ ((rnd + 1) & 1)];
+  unsigned int* const claim = &S.cnt[rnd == 0 ? 4 : 7 + rnd];
+  unsigned int* const next_n = &S.cnt[11 + rnd];
+  const unsigned int na = rnd == 0 ? S.cnt[2 + in] : S.cnt[11 + rnd - 1];
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
@@ -1655,14 +1726,14 @@ void wf_finish(const WFParams W) {
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
       unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(&S.cnt[4], want);
+      if (lane == 0) base = atomicAdd(claim, want);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
       const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
 #ifdef RT_FINISH_PROF
       if (base < na) prof_paths += min(want, na - base);
 #endif
       if (st == FS_IDLE && idx < na) {
-        path = S.active[in][idx];
+        path = list[idx];
         const uint32_t flags = S.s5[path].y & 0xffu;
         st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
         begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
@@ -1670,6 +1741,8 @@ void wf_finish(const WFParams W) {
       drained = base + want >= na;
     }
     if (!__any(st != FS_IDLE)) break;
+    // this wave hands its paths over to the next round at their next bounce
+    const bool handoff = drained && W.fin_handoff > 0 && __popcll(__ballot(st != FS_IDLE)) < W.fin_handoff;
     {  // fuller waves issue first (s_setprio by the lanes holding a path; see RT_FINISH_PRIO)
       const int busy = __popcll(__ballot(st != FS_IDLE));
       if (busy > RT_FINISH_PRIO) __builtin_amdgcn_s_setprio(3);
@@ -1718,9 +1791,15 @@ void wf_finish(const WFParams W) {
 #else
       const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, nsamples);
 #endif
+      const bool more = sh && (o.qShadow || o.qCont);
+      // (wave-uniform call: the wave's handed-over paths take one atomic)
+      const unsigned int hslot = wave_append(next_n, handoff && more);
       if (sh) {
         nsteps++;
-        if (o.qShadow || o.qCont) {
+        if (more && handoff) {
+          next_list[hslot] = path;
+          st = FS_IDLE;
+        } else if (more) {
           st = FS_TRACE;
           begin_rays(o.qShadow, o.qCont);
         } else {

@@ -38,3 +38,39 @@ def test_exact_edge_fallback_everywhere_keeps_the_full_hd_image(gpu_renderer, gp
     monkeypatch.setenv("RT_TRI_MARGIN_SCALE", "0")
     zero, _ = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
     print(f"{name}: zero margin: {int(bit_mismatch(zero, ref)[1].sum())} of {W * H} pixels differ")
+
+
+def test_zero_margin_fails_on_the_shared_edge_scene(gpu_renderer, gpu_dev_renderer, env_maps, monkeypatch):
+    """The negative control, asserted: tests/edge_cases.py aims the diagonal pixels'
+    camera rays exactly at a shared edge.  The release build equals the oracle bit for bit (the
+    reference's edge functions reject both triangles, the rays reach the back wall); the dev build
+    with the margin forced to 0 trusts the barycentric rows there and returns the quad instead, on
+    most of the diagonal's pixels."""
+    import numpy as np
+
+    import oracle as orc
+    from edge_cases import diagonal_frame_params, diagonal_scene
+    sc = diagonal_scene()
+    W = H = 128
+    fp = diagonal_frame_params(W)
+    ro = cf.rand_origins(2)
+    frames = [cf.oracle_frame_params(fp, k + 1, ro[k]) for k in range(2)]
+    ref, cnt = orc.render(orc.OracleScene(sc["tri_enc"], sc["node_enc"], env_maps[0], env_maps[1]), frames, W, H)
+
+    def render(r):
+        r.set_scene_encoded(sc["tri_enc"], sc["node_enc"])
+        r.set_env(env_maps[0], env_maps[1])
+        r.resize(W, H)
+        r.set_loop_num(0)
+        r.reset_stats()
+        st = r.render(fp, ro)
+        return r.read_accum(), st
+
+    img, st = render(gpu_renderer)
+    assert st["rays"] == cnt["rays"] and bit_mismatch(img, ref)[0] == 0.0
+    monkeypatch.setenv("RT_TRI_MARGIN_SCALE", "0")
+    bad, _ = render(gpu_dev_renderer)
+    diff = bit_mismatch(bad, ref)[1]
+    assert int(diff.sum()) > W // 2, int(diff.sum())
+    ys, xs = np.nonzero(diff)
+    assert np.all(np.abs(xs - ys) <= 1)  # on the diagonal (the rows' rounding is only wrong there)

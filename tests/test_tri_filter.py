@@ -60,7 +60,44 @@ def exact_inside(tri, P):
 
 
 def _fma(a, b, c):
-    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+    """fp32 fmaf(a, b, c) correctly rounded (rounding a*b + c to float64 and then to
+    float32 rounds twice).  The float64 product of two floats is exact; the float64 sum is rounded
+    to odd (TwoSum gives its exact error; an inexact sum with an even last bit moves one ulp toward
+    the exact value), and a round-to-odd result with 29 extra bits rounds to the float32 nearest the
+    exact a*b + c (Boldo & Melquiond)."""
+    p = a.astype(np.float64) * b.astype(np.float64)
+    c = np.broadcast_to(c, p.shape).astype(np.float64)
+    s = p + c
+    bb = s - p
+    err = (p - (s - bb)) + (c - bb)
+    bits = s.view(np.int64).copy()
+    fix = (err != 0) & ((bits & 1) == 0)
+    up = (err > 0) == (s > 0)  # the exact value lies away from zero
+    bits[fix] += np.where(up[fix], 1, -1)
+    return bits.view(np.float64).astype(f32)
+
+
+def test_fma_restatement_rounds_once():
+    """_fma against exact rational arithmetic, including cases built so that the float64 sum lands
+    on a float32 rounding midpoint (where rounding twice goes wrong)."""
+    from fractions import Fraction
+    rng = np.random.default_rng(5)
+    a = rng.uniform(-4, 4, 2000).astype(f32)
+    b = rng.uniform(-4, 4, 2000).astype(f32)
+    c = rng.uniform(-4, 4, 2000).astype(f32)
+    # midpoint cases: c = -(a*b) rounded, plus a tiny term, so the exact value sits next to a tie
+    half_ulp = f32(2.0) ** -25
+    a2 = np.array([1 + 2 ** -23, 1 + 3 * 2 ** -23, 3.0, 1 + 2 ** -12], f32)
+    b2 = np.array([1 + 2 ** -23, 1 - 2 ** -23, 1 + 2 ** -22, 1 + 2 ** -12], f32)
+    c2 = np.array([half_ulp, -half_ulp, f32(2.0 ** -24), f32(-2.0 ** -30)], f32)
+    A, B, Cc = (np.concatenate(x) for x in ((a, a2), (b, b2), (c, c2)))
+    got = _fma(A, B, Cc)
+    for x, y, z, g in zip(A, B, Cc, got):
+        exact = Fraction(float(x)) * Fraction(float(y)) + Fraction(float(z))
+        lo = f32(float(exact))
+        cands = [lo, np.nextafter(lo, f32(np.inf)), np.nextafter(lo, f32(-np.inf))]
+        best = min(cands, key=lambda v: (abs(Fraction(float(v)) - exact), int(np.asarray(v).view(np.uint32)) & 1))
+        assert g == best, (x, y, z, g, best)
 
 
 def filter_decision(rec, P, k1, k0):
@@ -171,3 +208,33 @@ def test_empty_and_degenerate_triangles():
     tri = _tri_records(p[:, 0], p[:, 1], p[:, 2])
     out, _, _, flagged = sl.tri_filter(tri)
     assert flagged == 1 and not out[:, 1:, :3].any()
+
+
+def test_diagonal_scene_probes_the_margin():
+    """tests/edge_cases.py: the camera rays of the diagonal pixels hit the shared edge exactly.  The
+    reference's edge test rejects both triangles there; the filter with the derived margin is never
+    decisive against it, and with the margin forced to 0 it contradicts it for most of those pixels
+    (the scene tests/test_gpu_tri_filter.py renders as the GPU negative control)."""
+    from edge_cases import diagonal_camera_rays, diagonal_scene
+    from test_cull_bound import geometric_normal, hit_triangle
+    sc = diagonal_scene()
+    W = 128
+    d = diagonal_camera_rays(W)
+    assert np.array_equal(d[:, 0], d[:, 1])
+    S = np.tile(np.array([0, 0, 3], f32), (W, 1))
+    p1, p2, p3 = (np.stack([t[k] for t in sc["tris"][:2]]) for k in range(3))
+    tri = _tri_records(p1, p2, p3)
+    rec, k1, k0, _ = sl.tri_filter(tri)
+    wrong = 0
+    for k in range(2):
+        q = [np.repeat(x[k:k + 1], W, 0) for x in (p1, p2, p3)]
+        ok, t = hit_triangle(*q, geometric_normal(*q), S, d)
+        assert not ok.any()  # the reference: neither triangle (the edge function is exactly 0)
+        P = (S + d * t[:, None]).astype(f32)
+        assert np.array_equal(P[:, 0], P[:, 1])
+        r = np.repeat(rec[k:k + 1], W, 0)
+        dec, ins = filter_decision(r, P, k1, k0)
+        assert not (dec & ins).any()
+        dec0, ins0 = filter_decision(r, P, 0.0, 0.0)
+        wrong += int((dec0 & ins0).sum())
+    assert wrong > W // 2, wrong
