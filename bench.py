@@ -6,7 +6,7 @@ HDR-environment MIS, camera/material/RNG exactly as the reference (rtamd/configs
 One *step* = ``--frames-per-step`` (default 1024 = the C3 config's spp)
 progressive frames (1 spp each) of the whole frame, rendered by one rt_render call per rank
 over that rank's pixel tiles with as many frames in flight as HBM holds (rt_set_max_paths:
-192 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 206 GB of path
+184 B per pixel-frame; one GPU runs the step as two launches of 512 frames = 206 GB of path
 state each, 8 tile-sharded GPUs run it as one launch of 1024 frames = 51 GB per rank),
 followed by the frame-end gather of every rank's fp32 accumulation tiles to rank 0 (RCCL over
 xGMI via torch.distributed, backend "nccl") and the un-permute into the full frame on rank 0.
@@ -52,12 +52,13 @@ SPEC_CLOCK_GHZ = 2.4      # max engine clock (MI355X_MICROARCH.md chip-level par
 B_INT, B_LEAF, B_TRI, B_UPD, B_ENV, B_CACHE, B_PIXEL = 64, 16, 36, 132, 12, 12, 24
 # wf_trace's own HBM stream per ray (the ~25 MB scene stays in L2 / Infinity Cache): a
 # secondary ray reads its 4-B queue entry and its 24-B origin/direction (WFState ra/rb or sa/sb:
-# {o.xyz, d.x} float4 + {d.y, d.z} float2) and writes its 8-B result; a camera ray is rebuilt from
-# the per-pixel camera table (16 B per pixel, shared by the pixel's frames) and writes its 8-B
-# result; pass 1's rays (rt_stats.p1_rays) are 16-B records {d, scattering distance} whose origin
-# is the pixel's camera hit point (WFState org, 16 B per pixel, shared by the pixel's frames)
-# (tests/test_bench_cpu.py pins these to the WFState layout)
-B_RAY_SECONDARY, B_RAY_PASS1, B_RAY_CAMERA = 4 + 24 + 8, 4 + 16 + 8, 8
+# {o.xyz, d.x} float4 + {d.y, d.z} float2) and writes its 4-B result (the closest triangle; the
+# shade recomputes t); a camera ray is rebuilt from the per-pixel camera table (16 B per pixel,
+# shared by the pixel's frames) and writes its 4-B result; pass 1's rays (rt_stats.p1_rays) are
+# 16-B records {d, scattering distance} whose origin is the pixel's camera hit point (WFState org,
+# 16 B per pixel, shared by the pixel's frames) (tests/test_bench_cpu.py pins these to the WFState
+# layout)
+B_RAY_SECONDARY, B_RAY_PASS1, B_RAY_CAMERA = 4 + 24 + 4, 4 + 16 + 4, 4
 # wf_trace's own traversal bytes per visit (served from L2 / MALL): a 128-B 4-wide node, a
 # 48-B triangle record
 B_QNODE, B_TRI_REC = 128, 48
@@ -243,17 +244,17 @@ def load_profile(config: str, W: int, H: int, F: int, slots: int):
 # wf_shade's algorithmic HBM bytes per path step (one path shaded in one bounce pass; rt_wavefront.h
 # shade_path, path-state layout DESIGN.md §3), for a path that continues with a shadow ray and a
 # continuation.  Passes >= 2: it reads its active-list entry (4 B), s5 (8), s0 + s2 (32), its two
-# 8-B results (16) and its 24-B continuation ray = 84 B, and writes s0 + s2 + s5 (40), the next
+# 4-B results (8) and its 24-B continuation ray = 76 B, and writes s0 + s2 + s5 (40), the next
 # continuation and shadow rays (2 x 24), two queue entries and an active entry (12) = 100 B.
-# Pass 0 (implicit camera paths): reads only the camera ray's 8-B result and writes the 16-B ray
-# records {d, s} of pass 1 (2 x 16) = 8 + 84 B.  Pass 1: reads the 16-B continuation record
-# instead of 24 B = 76 + 100 B.  The s1 / s3 / s4 rows (Lo, NEE, medium terms) are not counted
+# Pass 0 (implicit camera paths): reads only the camera ray's 4-B result and writes the 16-B ray
+# records {d, s} of pass 1 (2 x 16) = 4 + 84 B.  Pass 1: reads the 16-B continuation record
+# instead of 24 B = 68 + 100 B.  The s1 / s3 / s4 rows (Lo, NEE, medium terms) are not counted
 # (PF_ZLO paths skip them), nor the final colour of finishing paths.  Path steps per pass come
 # from the device (rt_stats.pass0_steps / pass1_steps / path_steps; the finisher's steps,
 # rt_stats.finish_steps, run in wf_finish and are not wf_shade's).
-B_SHADE_STEP = 84 + 100
-B_SHADE_P0 = 8 + 40 + 2 * 16 + 12
-B_SHADE_P1 = 76 + 100
+B_SHADE_STEP = 76 + 100
+B_SHADE_P0 = 4 + 40 + 2 * 16 + 12
+B_SHADE_P1 = 68 + 100
 VALU_PEAK_G = N_SIMD * SPEC_CLOCK_GHZ / VALU_CYC  # G wave64-VALU-instructions/s (2 cycles each per SIMD)
 
 
@@ -513,7 +514,7 @@ def main(argv=None) -> int:
     if pipelined:
         r.set_pipeline(args.pipeline)
     ad = r.accum_device()
-    # path-state budget: a whole step's frames in flight at once (192 B per pixel-frame: 51 GB
+    # path-state budget: a whole step's frames in flight at once (184 B per pixel-frame: 51 GB
     # per rank for 1024 frames of 1080p at N = 8); the library halves the frames per launch
     # until the state fits (512 = 206 GB of HBM3E on one GPU)
     path_slots = F * ad["local_tiles"] * args.tile * args.tile

@@ -56,7 +56,7 @@ enum {
   RT_ERR_LIMIT = -6     /* scene exceeds a kernel limit (leaf > 16 tris, depth > 64) */
 };
 
-/* Frames per kernel batch; the path-state budget (192 B per pixel-frame; rt_set_max_paths or
+/* Frames per kernel batch; the path-state budget (184 B per pixel-frame; rt_set_max_paths or
  * RT_MAX_SLOTS, default 320 Mi slots = 64 GB) bounds it too: 161 frames at 1920x1080 with the
  * default budget; bench.py raises the budget to a whole 1024-frame step, which one GPU runs as two
  * launches of 512 frames (206 GB) and each of 8 tile-sharded GPUs as one launch (51 GB). */
@@ -174,7 +174,7 @@ int rt_tile_costs(rt_ctx* ctx, const rt_frame_params* params, const float* rand_
  * unchanged (pixels are independent; the accumulation keeps its layout); rt_resize and
  * rt_set_tile_owners restore the natural order. */
 int rt_order_work(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames);
-/* Path-state budget in pixel-frames (192 B each): frames in flight per launch = slots / pixels of
+/* Path-state budget in pixel-frames (184 B each): frames in flight per launch = slots / pixels of
  * this rank, at most RT_MAX_FRAMES_PER_LAUNCH.  0 = RT_MAX_SLOTS from the environment or the
  * default 320 Mi slots.  A budget beyond free device memory runs fewer frames at a time.  No GL
  * counterpart: the fragment shader has one path per pixel in flight. */

@@ -784,14 +784,14 @@ constexpr size_t kMaxPendingEvents = 4096;
 // amortise the per-pass latency floor of the few longest rays (C3 1080p: 16 frames 1.07, 64
 // frames 0.94 ms/frame; 161 vs 80 frames +1.8%, all 512 of a bench step at once +2.2%).
 void update_frames_cap(rt_ctx* c, size_t nv) {
-  size_t max_slots = size_t(320) << 20;  // 192 B each: 64 GB of the 288 GB HBM3E
+  size_t max_slots = size_t(320) << 20;  // 184 B each: 62 GB of the 288 GB HBM3E
   if (const char* e = knob("RT_MAX_SLOTS")) max_slots = (size_t)strtoull(e, nullptr, 10);
   if (c->max_slots_req) max_slots = c->max_slots_req;
   c->frames_cap = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, max_slots / std::max<size_t>(1, nv)));
 }
 
 // Path-state buffers of the wavefront path: `paths` slots for each of the n_groups frame
-// groups, carved from one allocation (192 B per slot + counters).  RT_ERR_NOMEM when HBM
+// groups, carved from one allocation (184 B per slot + counters).  RT_ERR_NOMEM when HBM
 // cannot hold them (the caller then runs fewer frames at a time).
 static_assert(rt_ctx::MAX_GROUPS <= 4, "rtd::GroupCounters holds 4 groups' counters");
 int alloc_wavefront(rt_ctx* c, size_t paths) {
@@ -802,7 +802,7 @@ int alloc_wavefront(rt_ctx* c, size_t paths) {
     c->wf_mem = nullptr;
   }
   const size_t P = std::max<size_t>(paths, 64);
-  const size_t per = P * (5 * 16 + sizeof(*c->wfg[0].s5) + 2 * (16 + 8) + 16 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
+  const size_t per = P * (5 * 16 + sizeof(*c->wfg[0].s5) + 2 * (16 + 8) + 2 * 4 + 16 + 2 * 8 + 2 * 4) + 32768;  // + carve padding
   const hipError_t me = hipMalloc(&c->wf_mem, per * c->n_groups);
   if (me == hipErrorOutOfMemory) {
     (void)hipGetLastError();
@@ -819,7 +819,7 @@ int alloc_wavefront(rt_ctx* c, size_t paths) {
     w.s3 = (float4*)carve(P * 16); w.s4 = (float4*)carve(P * 16); w.s5 = (decltype(w.s5))carve(P * sizeof(*w.s5));
     w.ra = (float4*)carve(P * 16); w.rb = (float2*)carve(P * 8);
     w.sa = (float4*)carve(P * 16); w.sb = (float2*)carve(P * 8);
-    w.res = (int2*)carve(P * 16);
+    w.res = (int*)carve(P * 8);
     w.fin = (float4*)carve(P * 16);
     w.queue[0] = (int*)carve(P * 8); w.queue[1] = (int*)carve(P * 8);
     w.active[0] = (int*)carve(P * 4); w.active[1] = (int*)carve(P * 4);

@@ -63,7 +63,10 @@ struct WFState {
   float2* __restrict__ rb;
   float4* __restrict__ sa;
   float2* __restrict__ sb;
-  int2* __restrict__ res;    // per path: [2*p + 0] continuation (tri, t bits), [2*p + 1] shadow
+  // per path: [2*p + 0] the continuation's closest triangle, [2*p + 1] the shadow ray's (-1: none).
+  // The hit distance is not stored: the shade recomputes t from that triangle and the ray with the
+  // traversal's own operations (RT:265), the same bits (4 B per ray written instead of 8)
+  int* __restrict__ res;
   float4* __restrict__ fin;  // per path: final radiance curColor (RT:1549) awaiting the blend
   const unsigned int* __restrict__ pix_xy;   // per work item: px | py << 16
   const unsigned int* __restrict__ pix_acc;  // per work item: accumulation index
@@ -886,7 +889,7 @@ void wf_trace(const WFParams W) {
     if (!P.has_scene && MODE != MODE_SLOWIN) {  // empty scene: every ray misses (RT:346 reads a zero node)
       for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
         const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
-        S.res[e] = make_int2(-1, 0);
+        S.res[e] = -1;
       }
     }
     return;
@@ -1078,7 +1081,7 @@ void wf_trace(const WFParams W) {
       busy = false;
     }
     if (busy && finished) {
-      S.res[entry] = make_int2(L.besttri, __float_as_int(L.bestt));
+      S.res[entry] = L.besttri;
       if (COUNT) {
         if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
           const unsigned int w = (unsigned int)(entry >> 1) / (unsigned int)P.n_frames;
@@ -1150,7 +1153,7 @@ constexpr int SH_KEYS = 2;  // 0: no continuation hit (env / end of path); 1: a 
 // the hit material
 RTD int shade_key(const KParams& P, const WFState& S, int path) {
   const uint32_t flags = S.s5[path].y & 0xffu;
-  const int t = S.res[2 * path].x;
+  const int t = S.res[2 * path];
   if (!(flags & PF_CONT) || t < 0) return 0;
   return 1;
 }
@@ -1196,7 +1199,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     }
     // every load of the path's state issues at once: camera paths exist only in pass 0 (a
     // uniform test), so no load waits for the flags; the flags still decide what is used
-    int2 rsh = make_int2(0, 0);
+    int rsh = 0;
     if (loadPrev) {
       a0 = S.s0[path]; a2 = S.s2[path];
       rsh = S.res[2 * path + 1];
@@ -1209,7 +1212,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
         a3 = S.s3[path];
       }
     }
-    const int2 rc0 = S.res[2 * path];
+    const int rc0 = S.res[2 * path];
     float4 oo0, dd0;
     if (camPass) {
       oo0 = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
@@ -1234,7 +1237,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       Le0 = mk3(a1.w, a2.w, 0.0f);
       Le0.z = a3.w;
       // ---- pending NEE of the previous bounce (RT:1389-1405): add if the shadow ray escaped
-      if ((flags & PF_SHADOW) && rsh.x < 0) Lo = Lo + xyz(a3);
+      if ((flags & PF_SHADOW) && rsh < 0) Lo = Lo + xyz(a3);
       // ---- pending medium-emissive term (RT:1437-1439)
       if (flags & PF_CMED) {
         a4 = S.s4[path];
@@ -1245,22 +1248,23 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       fin = Le0 + Lo;
       doFinish = true;
     } else {
-      const int2 r = rc0;
+      const int r = rc0;
       const float4 oo = oo0, dd = dd0;
       const f3 ro = xyz(oo), rd = xyz(dd);
-      if (r.x >= 0) {
-        int tri = r.x;
+      if (r >= 0) {
+        int tri = r;
 #ifdef RT_CHECK
         if (tri >= P.n_tri) {
-          printf("[rt check] shade: path %d pass %d result triangle %d of %d (t bits %x)\n", path, W.pass, tri, P.n_tri, r.y);
+          printf("[rt check] shade: path %d pass %d result triangle %d of %d\n", path, W.pass, tri, P.n_tri);
           tri = 0;
         }
 #endif
-        const float t = __int_as_float(r.y);
         const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
         const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
         const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
         const f3 ng = mk3(A.w, B.w, Cc.w);
+        // t of the closest hit (RT:265): tl_triangle_calc's operations on the same ray and triangle
+        const float t = (dot(ng, p1) - dot(ro, ng)) / dot(rd, ng);
         const bool inside = dot(ng, rd) > 0.0f;
         const f3 Pp = ro + rd * t;
         const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
@@ -1765,7 +1769,7 @@ void wf_finish(const WFParams W) {
       }
 #endif
       if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
-        S.res[2 * path + (L.anyhit ? 1 : 0)] = make_int2(L.besttri, __float_as_int(L.bestt));
+        S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
         nrays++;
         if (contNext) begin_cont();
         else st = FS_SHADE;

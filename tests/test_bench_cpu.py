@@ -87,16 +87,16 @@ def test_bench_launcher_stops_the_other_ranks_when_one_fails():
 
 def test_trace_ray_bytes_follow_the_path_state_layout():
     """bench.py's algorithmic bytes per secondary ray = queue entry + the WFState ray rows
-    (float4 {o.xyz, d.x} + float2 {d.y, d.z}) + the 8-B result (the constant had
-    kept the 32-B ray of an older layout)."""
+    (float4 {o.xyz, d.x} + float2 {d.y, d.z}) + the 4-B result (the closest triangle; ADVICE r2:
+    the constant had kept the 32-B ray of an older layout)."""
     import bench
     src = (ROOT / "opengl-ray-tracing-framework_amd" / "csrc" / "hip" / "rt_wavefront.h").read_text()
     assert "float4* __restrict__ ra;" in src and "float2* __restrict__ rb;" in src
     assert "float4* __restrict__ sa;" in src and "float2* __restrict__ sb;" in src
-    assert "int2* __restrict__ res;" in src
-    assert bench.B_RAY_SECONDARY == 4 + (16 + 8) + 8
-    assert bench.B_RAY_PASS1 == 4 + 16 + 8  # WFState ra/sa float4 only (p1_ray): origin from org
-    assert bench.B_RAY_CAMERA == 8
+    assert "int* __restrict__ res;" in src
+    assert bench.B_RAY_SECONDARY == 4 + (16 + 8) + 4
+    assert bench.B_RAY_PASS1 == 4 + 16 + 4  # WFState ra/sa float4 only (p1_ray): origin from org
+    assert bench.B_RAY_CAMERA == 4
 
 
 def test_roofline_bound_follows_the_limiter():
@@ -116,8 +116,8 @@ def test_roofline_bound_follows_the_limiter():
         "wf_shade": {"avg_launch_ms": 13.0, "avg_launch_ms_standalone": 6.0, "hbm_bytes_per_launch": 3.0e10}}}
     r = bench.roofline(st, vis, None, prof, probe, 2)
     assert r["kernel"] == "wf_trace" and r["avg_launch_ms"] == 12.0 and "standalone" in r["avg_launch_ms_regime"]
-    # algorithmic bytes of the probe's launches: 8 B per camera ray, 36 B per other secondary ray
-    assert r["hbm"]["algorithmic_bytes_per_launch"] == round((8 * 400e6 + 36 * 600e6) / 5)
+    # algorithmic bytes of the probe's launches: 4 B per camera ray, 32 B per other secondary ray
+    assert r["hbm"]["algorithmic_bytes_per_launch"] == round((4 * 400e6 + 32 * 600e6) / 5)
     r1 = bench.roofline(st, vis, None, prof, dict(probe, p1_rays=50_000_000), 2)
     assert r["hbm"]["algorithmic_bytes_per_launch"] - r1["hbm"]["algorithmic_bytes_per_launch"] == 10_000_000 * 8
     want = 6.6e9 * 2 / (1024 * 2.4e9 * 12e-3)
@@ -128,7 +128,7 @@ def test_roofline_bound_follows_the_limiter():
     assert all(0 < v < 1 for v in r["utilisation"].values())
     sh = r["kernels"]["wf_shade"]
     assert sh["path_steps_per_launch"] == 100_000_000
-    assert sh["algorithmic_bytes_per_launch"] == round((92 * 200e6 + 176 * 300e6 + 184 * 500e6) / 10)
+    assert sh["algorithmic_bytes_per_launch"] == round((88 * 200e6 + 168 * 300e6 + 176 * 500e6) / 10)
     assert 0 < sh["frac"] < sh["traffic_frac"] < 1
     # per-step kernel time implied by each per-launch figure stays within the step
     assert r["avg_launch_ms"] * r["launches_per_step"] <= st["trace_ms"] / 2 * 1.0001
