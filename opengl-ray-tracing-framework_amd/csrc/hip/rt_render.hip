@@ -672,22 +672,23 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
   // pass 1 reads the 16-B rays pass 0 queued (WFState::org) in an instantiation of its own, so the
   // later passes' kernel carries none of it
   const bool p1 = !WP.cam_n && WP.pass == 1 && WP.p1_compact;
-  if (!COUNT && WIDE && c->fast_trace) {
+  if (WIDE && c->fast_trace) {
     // fast traversal, then the exact kernel over the rays it deferred (zero direction components,
-    // exact distance ties: usually none, and its blocks exit at once)
+    // exact distance ties: usually none, and its blocks exit at once).  COUNT: the visit counts
+    // (and the tile-cost probes) are those of the traversal that runs
     constexpr int F = rtd::MODE_FAST, SL = rtd::MODE_SLOWIN;
-    if (small) {  // static first shares of mid-size passes
+    if (small && !COUNT) {  // static first shares of mid-size passes
       if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
       else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true, F>), grid, dim3(256), c->trace_lds, st, WP);
       else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
     } else {
-      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, true, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, true, F>), grid, dim3(256), c->trace_lds, st, WP);
+      else hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
     }
-    if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
-    else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, SL>), grid, dim3(256), c->trace_lds, st, WP);
-    else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, true, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    else if (p1) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, true, SL>), grid, dim3(256), c->trace_lds, st, WP);
+    else hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
     return;
   }
   if (small && !COUNT && WIDE) {  // static first shares of mid-size passes

@@ -873,7 +873,7 @@ enum { MODE_EXACT = 0, MODE_FAST = 1, MODE_SLOWIN = 2 };
 template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false, int MODE = MODE_EXACT>  // P1: pass 1's 16-B rays
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
-  static_assert(MODE == MODE_EXACT || (WIDE && !COUNT), "fast / slow-list modes: 4-wide tree, no visit counting");
+  static_assert(MODE == MODE_EXACT || WIDE, "fast / slow-list modes: 4-wide tree");
   static_assert(MODE != MODE_SLOWIN || !STATIC, "the slow list is claimed dynamically");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
@@ -1013,6 +1013,7 @@ void wf_trace(const WFParams W) {
       // one triangle of the current leaf and one node step, then the iteration's single pop: a
       // taken leaf, or the node's nearest kept child (the top of the stack after the pushes)
       if (L.tri_i < L.tri_end) {
+        if (COUNT) { v_tri++; ray_steps++; }
         const int h = tl_triangle_fast(P, L, L.tri_i++);
         if (h == 2) {
           finished = defer = true;
@@ -1025,6 +1026,7 @@ void wf_trace(const WFParams W) {
       if (!finished && L.haveCur) {
         if (ref_is_leaf(L.cur)) {
           if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
+            if (COUNT) { v_leaf++; v_park++; }
             L.tri_i = leaf_first(L.cur);
             L.tri_end = L.tri_i + leaf_count(L.cur);
 #ifdef RT_CHECK
@@ -1036,6 +1038,7 @@ void wf_trace(const WFParams W) {
             needPop = true;
           }
         } else {
+          if (COUNT) { v_int++; ray_steps++; }
           tl_qnode_fast(P, L, TS, cull);
           needPop = true;
         }
