@@ -840,6 +840,39 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
   return tl_dual_calc(P, L, TS, cull, tl_dual_load(P, L, true));
 }
 
+// The finisher's fast step (RT_FINISH_FAST): wf_trace MODE_FAST's iteration for one lane (a
+// triangle, a node with octant-ordered pushes, the single pop); 0 going on, 1 done, 2 the ray must be
+// traced by the exact step (an exact distance tie).
+RTD int tl_step_fast(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull) {
+  bool finished = false;
+  if (L.tri_i < L.tri_end) {
+    const int h = tl_triangle_fast(P, L, L.tri_i++);
+    if (h == 2) return 2;
+    if (h == 1 && L.anyhit) {
+      finished = true;
+      L.tri_end = L.tri_i;
+    }
+  }
+  bool needPop = false;
+  if (!finished && L.haveCur) {
+    if (ref_is_leaf(L.cur)) {
+      if (L.tri_i >= L.tri_end) {
+        L.tri_i = leaf_first(L.cur);
+        L.tri_end = L.tri_i + leaf_count(L.cur);
+        needPop = true;
+      }
+    } else {
+      tl_qnode_fast(P, L, TS, cull);
+      needPop = true;
+    }
+  }
+  if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
+  return (finished || (!L.haveCur && L.tri_i >= L.tri_end)) ? 1 : 0;
+}
+#ifndef RT_FINISH_FAST
+#define RT_FINISH_FAST 0
+#endif
+
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
 #endif
@@ -1696,6 +1729,7 @@ void wf_finish(const WFParams W) {
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
+  bool exact = !RT_FINISH_FAST;  // (RT_FINISH_FAST) this lane's ray runs the exact step
   TraceLane L;
   L.anyhit = false;
   // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation, whose
@@ -1715,6 +1749,7 @@ void wf_finish(const WFParams W) {
     L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
     L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
     tl_start<WIDE>(P, L);
+    if (RT_FINISH_FAST) exact = !WIDE || !L.finite;
   };
   auto begin_cont = [&]() {
     if (!RT_FINISH_HOLD_CONT) {
@@ -1726,6 +1761,7 @@ void wf_finish(const WFParams W) {
     L.ox = ca.x; L.oy = ca.y; L.oz = ca.z;
     L.dx = ca.w; L.dy = cb.x; L.dz = cb.y;
     tl_start<WIDE>(P, L);
+    if (RT_FINISH_FAST) exact = !WIDE || !L.finite;
   };
   while (true) {
     // idle lanes take the next paths of the active list (one atomic per wave)
@@ -1771,7 +1807,22 @@ void wf_finish(const WFParams W) {
           if (!prof_at[q] && busy <= lim[q]) { prof_at[q] = wall_clock64(); prof_it_at[q] = prof_it; }
       }
 #endif
-      if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
+      bool done = false;
+      if (st == FS_TRACE) {
+        if (!P.has_scene) {
+          done = true;
+        } else if (!RT_FINISH_FAST || exact) {
+          done = tl_step_prefetch<WIDE>(P, L, TS, cull);
+        } else {
+          const int h = tl_step_fast(P, L, TS, cull);
+          if (h == 2) {  // an exact tie: the ray again, with the exact step
+            tl_start<WIDE>(P, L);
+            exact = true;
+          }
+          done = h == 1;
+        }
+      }
+      if (done) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
         nrays++;
         if (contNext) begin_cont();

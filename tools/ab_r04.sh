@@ -28,5 +28,6 @@ timeout -k 10 1200 python3 tools/ab_proc.py --frames 1024 --whole --reps 2 --rou
 tail -7 $O/ab.log
 timeout -k 10 900 python3 tools/ab_single.py --config C3 --rounds 3 head=$EXP/librtamd_head.so:RT_AB_ORDER=1 \
   r1=$DEV:RT_AB_ORDER=1,RT_FINISH_ROUNDS=1,RT_FAST_TRACE=1 r3=$DEV:RT_AB_ORDER=1,RT_FINISH_ROUNDS=3,RT_FAST_TRACE=1 \
+  ff=$EXP/librtamd_finfast.so:RT_AB_ORDER=1 \
   > $O/ab_single.log 2>&1 || { tail -20 $O/ab_single.log; exit 1; }
 tail -4 $O/ab_single.log
