@@ -600,7 +600,8 @@ def main(argv=None) -> int:
     probe = None
     if st["trace_launches"]:
         from rtamd.renderer import RT_FLAG_SERIAL
-        per_group = max(1, round(F * (fp.max_bounce + 1) * steps / st["trace_launches"]))
+        # (rt_stats.launches counts the batches a render call is split into; two frame groups each)
+        per_group = max(1, -(-F * steps // (2 * max(1, st["launches"]))))
         r.reset_stats()
         r.render(cf.frame_params(W, H, flags=RT_FLAG_SERIAL), ro[-1 - per_group:-1])
         probe = r.stats()

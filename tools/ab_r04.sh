@@ -15,10 +15,10 @@ if [ -z "$SKIP_CHK" ]; then
   if grep -q "rt check" $O/chk.log; then echo "bounds check fired"; exit 1; fi
 fi
 if [ -z "$SKIP_TESTS" ]; then
-  RTAMD_LIB=$PWD/$EXP/librtamd_fast.so RT_FAST_TRACE=1 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+  RTAMD_LIB=$PWD/$EXP/librtamd_fastrel.so RT_FAST_TRACE=1 RT_FINISH_ROUNDS=3 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
   tail -2 $O/tests.log
 fi
-for F in 0 1; do  # visit counts per ray of the exact and the fast traversal (C3 1080p, 4 frames)
+[ -z "$SKIP_VISITS" ] && for F in 0 1; do  # visit counts per ray of the exact and the fast traversal (C3 1080p, 4 frames)
   RTAMD_LIB=$PWD/$DEV RT_FAST_TRACE=$F RT_ORD_KEY=${ORD:-centre} timeout -k 10 300 python3 tools/quick_perf.py --frames 4 --count-frames 4 2>&1 | tail -1 | sed "s/^/fast=$F /"
   RTAMD_LIB=$PWD/$DEV RT_FAST_TRACE=$F RT_ORD_KEY=corner timeout -k 10 300 python3 tools/quick_perf.py --frames 4 --count-frames 4 2>&1 | tail -1 | sed "s/^/fast=$F corner /"
 done | tee $O/visits.log
