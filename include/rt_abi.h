@@ -107,8 +107,10 @@ enum {
   RT_FLAG_MEGAKERNEL = 4,         /* single persistent megakernel instead of the wavefront path */
   RT_FLAG_NO_FINISH = 8,          /* never end paths in the path-persistent finisher            */
   RT_FLAG_FINISH = 16,            /* use the finisher whatever the batch size (rt_set_finish)   */
-  RT_FLAG_SERIAL = 32             /* measurement: one frame group per batch (no two groups' kernels
+  RT_FLAG_SERIAL = 32,            /* measurement: one frame group per batch (no two groups' kernels
                                      overlap), at most one group's path state of frames per batch */
+  RT_FLAG_SORTED_TRAVERSAL = 64   /* wavefront trace: visit children by entry distance only (the exact
+                                     kernel alone, no octant-ordered fast traversal); same image */
 };
 
 typedef struct rt_stats {

@@ -99,6 +99,7 @@ struct rt_ctx {
 #define RT_FAST_TRACE_DEFAULT 0
 #endif
   bool fast_trace = RT_FAST_TRACE_DEFAULT;    // wf_trace MODE_FAST + MODE_SLOWIN (dev: RT_FAST_TRACE=0/1)
+  bool call_fast = false;                     // this call's launches: fast_trace && !RT_FLAG_SORTED_TRAVERSAL
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
@@ -139,12 +140,6 @@ struct rt_ctx {
   int finish_pass = 2;  // C3 1080p single frames: 1 / 2 / 3 -> 3.73 / 3.35 / 3.41 ms (off: 3.79)
   uint64_t finish_slots = uint64_t(8) << 20;
   int finish_bpc = 0;              // wf_finish blocks per CU
-  // wf_finish path compaction: rounds (launches) and the busy-lane count below which a drained
-  // wave hands its paths to the next round (rtd::wf_finish); 1 round = none
-#ifndef RT_FINISH_ROUNDS_DEFAULT
-#define RT_FINISH_ROUNDS_DEFAULT 1
-#endif
-  int finish_rounds = RT_FINISH_ROUNDS_DEFAULT, finish_handoff = 16;
   // Pipelined one-frame calls (rt_set_pipeline, depth D = 2): one-frame call k runs as a single
   // group on stream aux[1 + p], p = k mod D, with path-state set wfg[p], camera table p and frame
   // table ft[1 + p], so call k+1's early passes fill the CUs that call k's latency-bound finisher
@@ -529,10 +524,11 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
         hi[k][i] = i < (int)sl.size() ? sl[i].hi[k] : -pinf;
       }
     // fast traversal's child order per ray-direction octant o (bit a set: component a of the
-    // direction negative): children by the projection of their box centre onto the octant's
-    // diagonal, nearest first; ord[o] holds, in nibble c, the children that come after child c
-    // (dev RT_ORD_KEY=corner: by the box corner a ray of the octant enters first instead)
-    static const bool ord_corner = knob("RT_ORD_KEY") && strcmp(knob("RT_ORD_KEY"), "corner") == 0;
+    // direction negative): children by the projection onto the octant's diagonal, nearest first;
+    // ord[o] holds, in nibble c, the children that come after child c
+    // children by the box corner a ray of the octant enters first (dev RT_ORD_KEY=centre: by the
+    // box centre; C3 bulk -1.2%)
+    static const bool ord_corner = !(knob("RT_ORD_KEY") && strcmp(knob("RT_ORD_KEY"), "centre") == 0);
     uint16_t ord[8];
     for (int o = 0; o < 8; o++) {
       double key[4];
@@ -672,7 +668,7 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
   // pass 1 reads the 16-B rays pass 0 queued (WFState::org) in an instantiation of its own, so the
   // later passes' kernel carries none of it
   const bool p1 = !WP.cam_n && WP.pass == 1 && WP.p1_compact;
-  if (WIDE && c->fast_trace) {
+  if (WIDE && c->call_fast) {
     // fast traversal, then the exact kernel over the rays it deferred (zero direction components,
     // exact distance ties: usually none, and its blocks exit at once).  COUNT: the visit counts
     // (and the tile-cost probes) are those of the traversal that runs
@@ -854,8 +850,6 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
   if (const char* e = knob("RT_FAST_TRACE")) c->fast_trace = atoi(e) != 0;
-  if (const char* e = knob("RT_FINISH_ROUNDS")) c->finish_rounds = std::max(1, std::min(4, atoi(e)));
-  if (const char* e = knob("RT_FINISH_HANDOFF")) c->finish_handoff = std::max(0, std::min(64, atoi(e)));
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess || hipEventCreate(&c->t_ref) != hipSuccess ||
       hipEventRecord(c->t_ref, c->stream) != hipSuccess) {
@@ -1310,6 +1304,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
   const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
   const bool serial = (fp->flags & RT_FLAG_SERIAL) != 0 && !(fp->flags & RT_FLAG_MEGAKERNEL);
+  c->call_fast = c->fast_trace && !(fp->flags & RT_FLAG_SORTED_TRAVERSAL);
   bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && !serial && n_trace_pre > 0 &&
               c->n_valid >= 64 * c->n_groups && !c->tile_cost_on &&
               (n_trace_pre < c->n_groups ||
@@ -1579,8 +1574,6 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.n_frames = f1 - f0;
         WP.pass = 0;
         WP.cam_n = 0u;
-        WP.fin_round = 0;
-        WP.fin_handoff = 0;
         // (not for frame groups of one frame each: their blends must run in frame order)
         WP.fuse_blend = (!pipe && WP.n_frames == 1 && (pix_split || G == 1) && !count) ? 1 : 0;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
@@ -1638,21 +1631,14 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
               HIPCHK(c, hipEventRecord(ft0, sg[g]));
             }
 #endif
-            // rounds: waves that thin out hand their paths to the next round's full waves
-            const int rounds = std::max(1, std::min(4, c->finish_rounds));
-            for (int rnd = 0; rnd < rounds; rnd++) {
-              rtd::WFParams WR = WP;
-              WR.fin_round = rnd;
-              WR.fin_handoff = rnd + 1 < rounds ? c->finish_handoff : 0;
-              if (fp->enable_bsdf) {
-                if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
-                else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
-              } else {
-                if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<false, true>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
-                else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WR);
-              }
-              HIPCHK(c, hipGetLastError());
+            if (fp->enable_bsdf) {
+              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<true, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+              else hipLaunchKernelGGL((rtd::wf_finish<true, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+            } else {
+              if (c->wide) hipLaunchKernelGGL((rtd::wf_finish<false, true>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
+              else hipLaunchKernelGGL((rtd::wf_finish<false, false>), fgrid, dim3(256), c->trace_lds, sg[g], WP);
             }
+            HIPCHK(c, hipGetLastError());
 #ifdef RT_DEV
             if (debug_passes) {  // development aid: the finisher's waves (syncs!)
               HIPCHK(c, hipEventRecord(ft1, sg[g]));

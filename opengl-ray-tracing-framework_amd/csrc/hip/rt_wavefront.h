@@ -111,10 +111,6 @@ struct WFParams {
   // per group): a finishing path blends into the accumulation itself (wf_blend's operations,
   // RT:1552) instead of writing fin for a wf_blend launch after the last pass
   int fuse_blend;
-  // wf_finish rounds (path compaction): round fin_round of a finisher that runs as several launches;
-  // a round hands a path over to the next round (instead of starting its next bounce) once its
-  // wave has drained the round's list and holds fewer than fin_handoff paths (0: never)
-  int fin_round, fin_handoff;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -607,7 +603,11 @@ RTD void tl_store(const TraceStack& S, int idx, int2 ent) {  // the entry at sta
   if (idx < S.KL) S.lds[idx * TL_LANES] = ent;
   else *S.ovf_at(idx) = pack_ent(ent);
 }
-RTD void tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
+#ifndef RT_FAST_POP_NEAR  // 1: the nearest kept child is pushed too and taken by the single pop
+#define RT_FAST_POP_NEAR 0
+#endif
+// returns true when no child was entered (the caller pops)
+RTD bool tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
 #ifdef RT_CHECK
   if ((unsigned)L.cur >= (unsigned)P.n_qnodes) {
     printf("[rt check] fast node %d of %d (sp %d)\n", L.cur, P.n_qnodes, L.sp);
@@ -648,7 +648,15 @@ RTD void tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool
     for (int c = 0; c < 4; c++)
       if (ok[c]) tl_store(S, L.sp + f[c], make_int2(r[c], __float_as_int(t0[c])));
   }
-  L.sp += n;
+  if (RT_FAST_POP_NEAR) {
+    L.sp += n;
+    return true;
+  }
+  // the nearest kept child (position n - 1, stored above the new top) is entered at once
+  const int top = n - 1;
+  L.cur = f[0] == top ? r[0] : f[1] == top ? r[1] : f[2] == top ? r[2] : r[3];
+  L.sp += max(top, 0);
+  return n == 0;
 }
 #ifndef RT_FAST_DEFER_EDGES  // fast traversal: a point the edge filter cannot decide defers the ray (1) or
                              // runs the reference's edge functions in place (0)
@@ -839,39 +847,6 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
   if (!WIDE) return tl_dual_step<WIDE>(P, L, TS, cull);
   return tl_dual_calc(P, L, TS, cull, tl_dual_load(P, L, true));
 }
-
-// The finisher's fast step (RT_FINISH_FAST): wf_trace MODE_FAST's iteration for one lane (a
-// triangle, a node with octant-ordered pushes, the single pop); 0 going on, 1 done, 2 the ray must be
-// traced by the exact step (an exact distance tie).
-RTD int tl_step_fast(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull) {
-  bool finished = false;
-  if (L.tri_i < L.tri_end) {
-    const int h = tl_triangle_fast(P, L, L.tri_i++);
-    if (h == 2) return 2;
-    if (h == 1 && L.anyhit) {
-      finished = true;
-      L.tri_end = L.tri_i;
-    }
-  }
-  bool needPop = false;
-  if (!finished && L.haveCur) {
-    if (ref_is_leaf(L.cur)) {
-      if (L.tri_i >= L.tri_end) {
-        L.tri_i = leaf_first(L.cur);
-        L.tri_end = L.tri_i + leaf_count(L.cur);
-        needPop = true;
-      }
-    } else {
-      tl_qnode_fast(P, L, TS, cull);
-      needPop = true;
-    }
-  }
-  if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
-  return (finished || (!L.haveCur && L.tri_i >= L.tri_end)) ? 1 : 0;
-}
-#ifndef RT_FINISH_FAST
-#define RT_FINISH_FAST 0
-#endif
 
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
@@ -1072,8 +1047,7 @@ void wf_trace(const WFParams W) {
           }
         } else {
           if (COUNT) { v_int++; ray_steps++; }
-          tl_qnode_fast(P, L, TS, cull);
-          needPop = true;
+          needPop = tl_qnode_fast(P, L, TS, cull);
         }
       }
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
@@ -1684,15 +1658,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
 #define RT_FINISH_WPE 2
 #endif
-// Path compaction (rounds): once the list is drained, waves thin out to their few long bounce chains
-// (<= 16 busy lanes for about half of the finisher's wave time, 0.11 VALU lane utilisation).  So
-// the finisher runs as rounds: in every round but the last, a wave that has drained the round's
-// list and holds fewer than fin_handoff paths writes each path whose shade step just queued its
-// next rays to the next round's list (the path's state and rays are in memory at that point, as
-// for a path of the active list) instead of tracing them, and ends when its lanes are idle; the
-// next round starts those paths on full waves.  Round r reads list r and writes list r + 1:
-// active[in ^ (r & 1)], counts cnt[2 + in] (r = 0) and cnt[11 + r - 1], claims cnt[4] (r = 0) and
-// cnt[7 + r].
 template <bool BSDF, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FINISH_WPE)))
 void wf_finish(const WFParams W) {
@@ -1700,12 +1665,7 @@ void wf_finish(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1;
-  const int rnd = W.fin_round;
-  const int* const list = S.active[in ^ (rnd & 1)];
-  int* const next_list = S.active[in ^ ((rnd + 1) & 1)];
-  unsigned int* const claim = &S.cnt[rnd == 0 ? 4 : 7 + rnd];
-  unsigned int* const next_n = &S.cnt[11 + rnd];
-  const unsigned int na = rnd == 0 ? S.cnt[2 + in] : S.cnt[11 + rnd - 1];
+  const unsigned int na = S.cnt[2 + in];
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
@@ -1729,7 +1689,6 @@ void wf_finish(const WFParams W) {
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
-  bool exact = !RT_FINISH_FAST;  // (RT_FINISH_FAST) this lane's ray runs the exact step
   TraceLane L;
   L.anyhit = false;
   // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation, whose
@@ -1749,7 +1708,6 @@ void wf_finish(const WFParams W) {
     L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
     L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
     tl_start<WIDE>(P, L);
-    if (RT_FINISH_FAST) exact = !WIDE || !L.finite;
   };
   auto begin_cont = [&]() {
     if (!RT_FINISH_HOLD_CONT) {
@@ -1761,7 +1719,6 @@ void wf_finish(const WFParams W) {
     L.ox = ca.x; L.oy = ca.y; L.oz = ca.z;
     L.dx = ca.w; L.dy = cb.x; L.dz = cb.y;
     tl_start<WIDE>(P, L);
-    if (RT_FINISH_FAST) exact = !WIDE || !L.finite;
   };
   while (true) {
     // idle lanes take the next paths of the active list (one atomic per wave)
@@ -1769,14 +1726,14 @@ void wf_finish(const WFParams W) {
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
       unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(claim, want);
+      if (lane == 0) base = atomicAdd(&S.cnt[4], want);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
       const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
 #ifdef RT_FINISH_PROF
       if (base < na) prof_paths += min(want, na - base);
 #endif
       if (st == FS_IDLE && idx < na) {
-        path = list[idx];
+        path = S.active[in][idx];
         const uint32_t flags = S.s5[path].y & 0xffu;
         st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
         begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
@@ -1784,8 +1741,6 @@ void wf_finish(const WFParams W) {
       drained = base + want >= na;
     }
     if (!__any(st != FS_IDLE)) break;
-    // this wave hands its paths over to the next round at their next bounce
-    const bool handoff = drained && W.fin_handoff > 0 && __popcll(__ballot(st != FS_IDLE)) < W.fin_handoff;
     {  // fuller waves issue first (s_setprio by the lanes holding a path; see RT_FINISH_PRIO)
       const int busy = __popcll(__ballot(st != FS_IDLE));
       if (busy > RT_FINISH_PRIO) __builtin_amdgcn_s_setprio(3);
@@ -1807,22 +1762,7 @@ void wf_finish(const WFParams W) {
           if (!prof_at[q] && busy <= lim[q]) { prof_at[q] = wall_clock64(); prof_it_at[q] = prof_it; }
       }
 #endif
-      bool done = false;
-      if (st == FS_TRACE) {
-        if (!P.has_scene) {
-          done = true;
-        } else if (!RT_FINISH_FAST || exact) {
-          done = tl_step_prefetch<WIDE>(P, L, TS, cull);
-        } else {
-          const int h = tl_step_fast(P, L, TS, cull);
-          if (h == 2) {  // an exact tie: the ray again, with the exact step
-            tl_start<WIDE>(P, L);
-            exact = true;
-          }
-          done = h == 1;
-        }
-      }
-      if (done) {
+      if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
         nrays++;
         if (contNext) begin_cont();
@@ -1849,15 +1789,9 @@ void wf_finish(const WFParams W) {
 #else
       const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, nsamples);
 #endif
-      const bool more = sh && (o.qShadow || o.qCont);
-      // (wave-uniform call: the wave's handed-over paths take one atomic)
-      const unsigned int hslot = wave_append(next_n, handoff && more);
       if (sh) {
         nsteps++;
-        if (more && handoff) {
-          next_list[hslot] = path;
-          st = FS_IDLE;
-        } else if (more) {
+        if (o.qShadow || o.qCont) {
           st = FS_TRACE;
           begin_rays(o.qShadow, o.qCont);
         } else {

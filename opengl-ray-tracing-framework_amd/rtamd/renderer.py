@@ -25,6 +25,7 @@ RT_FLAG_MEGAKERNEL = 4
 RT_FLAG_NO_FINISH = 8
 RT_FLAG_FINISH = 16
 RT_FLAG_SERIAL = 32
+RT_FLAG_SORTED_TRAVERSAL = 64
 RT_ABI_VERSION = 4
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 

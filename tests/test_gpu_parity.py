@@ -11,12 +11,13 @@ import pytest
 
 from helpers import bit_mismatch, frames_for, gpu_render, oracle_render
 from rtamd import configs as cf
-from rtamd.renderer import RT_FLAG_MEGAKERNEL, RT_FLAG_NO_CULL
+from rtamd.renderer import RT_FLAG_MEGAKERNEL, RT_FLAG_NO_CULL, RT_FLAG_SORTED_TRAVERSAL
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("flags", [0, RT_FLAG_MEGAKERNEL], ids=["wavefront", "megakernel"])
+@pytest.mark.parametrize("flags", [0, RT_FLAG_SORTED_TRAVERSAL, RT_FLAG_MEGAKERNEL],
+                         ids=["wavefront", "wavefront-sorted", "megakernel"])
 @pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
 def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     sd = cf.config_scene(name)
@@ -28,7 +29,7 @@ def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     frac, _ = bit_mismatch(img, ref)
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert st["samples"] == cnt["samples"] == W * H * 2
-    if flags == 0:  # shade steps: one per path per pass, each after that path traced 1-2 rays
+    if not flags & RT_FLAG_MEGAKERNEL:  # shade steps: one per path per pass, each after that path traced 1-2 rays
         assert st["samples"] <= st["path_steps"] <= st["rays"], st
     assert frac == 0.0, f"{name}: {frac:.4%} of pixels differ from the oracle"
 
