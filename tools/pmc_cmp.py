@@ -24,7 +24,11 @@ for v in variants:
                      glob.glob(f"{root}/{v}/{p}/run_counter_collection.csv")):
             for r in csv.DictReader(open(f)):
                 cnt[kname(r)][r["Counter_Name"]] += float(r["Counter_Value"])
-    print(f"== {v}")
+    rays = 0
+    for ln in open(f"{root}/{v}.a.log", errors="replace"):
+        if ln.startswith("rays_total "):
+            rays = int(ln.split()[1])
+    print(f"== {v}" + (f"  ({rays} rays, every render of the run)" if rays else ""))
     for k in sorted(dur, key=lambda k: -dur[k]):
         if not k.startswith("wf_") and "rt_" not in k:
             continue
@@ -40,6 +44,9 @@ for v in variants:
             if c.get("SQ_WAVE_CYCLES"):
                 line += f"  wait {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.2f}"
             line += f"  vmem {c.get('SQ_INSTS_VMEM_RD', 0):.3e}  salu {c.get('SQ_INSTS_SALU', 0):.3e}"
+            if rays and k == "wf_trace":
+                line += (f"  per ray: valu {c['SQ_INSTS_VALU'] / rays:.1f} salu {c.get('SQ_INSTS_SALU', 0) / rays:.1f}"
+                         f"  salu/valu {c.get('SQ_INSTS_SALU', 0) / c['SQ_INSTS_VALU']:.2f}")
         if c.get("TCC_HIT_sum"):
             line += f"  L2hit {c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']):.3f}"
         print(line)

@@ -34,7 +34,7 @@ r.resize(W, H)
 print("device", r.device_info(), flush=True)
 fp = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=a.flags)
 ro = cf.rand_origins(a.frames + 1 + max(64, a.count_frames))
-r.render(fp, ro[:1])
+rays_total = r.render(fp, ro[:1])["rays"]
 r.reset_stats()
 t = time.time()
 k = 1
@@ -44,6 +44,7 @@ while k < a.frames + 1:
     k += n
 st = r.stats()
 wall = time.time() - t
+rays_total += st["rays"]
 ms = st["kernel_ms"] / a.frames
 print(f"{a.config} {W}x{H} mb={a.max_bounce} flags={a.flags}: {ms:.2f} ms/frame (kernel), wall {wall*1000/a.frames:.2f} ms/frame, "
       f"{st['rays']/st['kernel_ms']/1e3:.1f} Mrays/s, rays/frame {st['rays']/a.frames/1e6:.2f} M", flush=True)
@@ -51,7 +52,8 @@ fpc = cf.frame_params(W, H, max_bounce=a.max_bounce, flags=RT_FLAG_COUNT_VISITS 
 r.reset_stats()
 r.render(fpc, ro[-a.count_frames:])
 st = r.stats()
+rays_total += st["rays"]
 print("visits per ray: internal %.1f leaf %.1f tri %.1f; trace loop iters/wave-pass avg %.0f max %d (%d launches)" % (
       st["internal_pops"] / st["rays"], st["leaf_pops"] / st["rays"], st["tri_tests"] / st["rays"],
       st["trace_iters"] / max(1, st["trace_launches"]) / 3072, st["trace_iters_max"], st["trace_launches"]), flush=True)
-
+print(f"rays_total {rays_total}", flush=True)  # every render of the run (tools/pmc_cmp.py: per ray)
