@@ -383,6 +383,33 @@ RTD bool tl_edges_exact(const KParams& P, int i, const f3 p1, const f3 ng, const
 // b3 = R3.(P - p1), b1 = 1 - b2 - b3 whenever min(b) lies outside the error margin
 // m = k1 * max|P - p1| * (max|R2| + max|R3|) + k0 that bounds both b's error and the fp32 error of
 // the reference's edge functions (tri_filter.h derives it), else by those edge functions.
+// the hit test alone (no tie rule, L unchanged): true when triangle i is hit at dist <= L.best
+// (WIDE) / < L.best; dist = t - 0.00001 and t returned
+template <bool WIDE>
+RTD bool tl_tri_hit(const KParams& P, const TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc,
+                    float& dist_out, float& t_out) {
+  const f3 p1 = xyz(A);
+  const f3 ng = mk3(A.w, B.w, Cc.w);
+  const float dn = dot(ng, L.d());
+  const float num = dot(ng, p1) - dot(L.o(), ng);
+  const float t = num / dot(L.d(), ng);                                // RT:265
+  const float dist = t - 0.00001f;
+  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (WIDE ? dist <= L.best : dist < L.best);  // RT:262, 268, 328/356
+  const f3 Pp = L.o() + L.d() * t;
+  const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
+  const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
+  const float b3 = __builtin_fmaf(Cc.x, qx, __builtin_fmaf(Cc.y, qy, Cc.z * qz));
+  const float b1 = (1.0f - b2) - b3;
+  const float mn = fminf(b1, fminf(b2, b3));
+  const float dq = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
+  const float lr = fmaxf(fabsf(B.x), fmaxf(fabsf(B.y), fabsf(B.z))) + fmaxf(fabsf(Cc.x), fmaxf(fabsf(Cc.y), fabsf(Cc.z)));
+  const float m = (dq * lr) * P.tri_k1 + P.tri_k0;
+  bool inside = mn > 0.0f;
+  if (ok & !((fabsf(mn) > m) & (m < 0.25f))) inside = tl_edges_exact(P, i, p1, ng, Pp);
+  dist_out = dist;
+  t_out = t;
+  return ok & inside;
+}
 template <bool WIDE>
 RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
   // straight-line form: every condition of RT:262-281 folded into one predicate (a 64-lane wave
@@ -848,6 +875,148 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
   return tl_dual_calc(P, L, TS, cull, tl_dual_load(P, L, true));
 }
 
+// ---- cooperative traversal: four lanes per ray (wf_finish's drained waves, RT_FINISH_COOP).
+// The four lanes of a quad hold identical copies of one path's state (ray, best hit, cursors,
+// stack) and make identical decisions; only two parts are split: lane c of the quad tests child
+// box c of a 4-wide node, and triangle tri_i + c of the current leaf.  The quad's results are
+// exchanged with DPP quad broadcasts, so each lane then runs the usual push (its own stack copy)
+// and merges the four triangle candidates in index order with the sequential rules (dist <= best,
+// exact ties by tie_wins, an any-hit ray stops at its first accepted triangle): the same closest
+// hit as testing them one after the other.
+template <int K>
+RTD int quad_bcast(int x) {  // lane K of each quad, to all four
+  return __builtin_amdgcn_update_dpp(0, x, K | K << 2 | K << 4 | K << 6, 0xf, 0xf, false);
+}
+template <int K>
+RTD float quad_bcast(float x) {
+  return __int_as_float(quad_bcast<K>(__float_as_int(x)));
+}
+// node step: child c's box with the operations of tl_qnode_keys, then every lane pushes all four
+RTD bool tl_qnode_coop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, int c) {
+  const uint32_t off = ((uint32_t)L.cur << 7) + 4u * (uint32_t)c;
+#ifdef RT_CHECK
+  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) printf("[rt check] coop node %d of %d\n", L.cur, P.n_qnodes);
+#endif
+  const int ref = ld<int>(P.qnodes, off + 96u);
+  const float lim = cull ? L.limit(P.cull_eps) : __int_as_float(0x7f800000);
+  float t0, t1;
+  if (L.finite) {  // tl_qnode_t01 for one child
+    const float nx = ld<float>(P.qnodes, off + L.offNx), ny = ld<float>(P.qnodes, off + L.offNy),
+                nz = ld<float>(P.qnodes, off + L.offNz);
+    const float fx = ld<float>(P.qnodes, off + (48 - L.offNx)), fy = ld<float>(P.qnodes, off + (80 - L.offNy)),
+                fz = ld<float>(P.qnodes, off + (112 - L.offNz));
+    t0 = max_((nx - L.ox) * L.ix, max_((ny - L.oy) * L.iy, (nz - L.oz) * L.iz));
+    t1 = min_((fx - L.ox) * L.ix, min_((fy - L.oy) * L.iy, (fz - L.oz) * L.iz));
+  } else {  // the literal slab (tl_qnode_keys' generic case)
+    const f3 n = (mk3(ld<float>(P.qnodes, off), ld<float>(P.qnodes, off + 16u), ld<float>(P.qnodes, off + 32u)) - L.o()) * L.inv();
+    const f3 f = (mk3(ld<float>(P.qnodes, off + 48u), ld<float>(P.qnodes, off + 64u), ld<float>(P.qnodes, off + 80u)) - L.o()) * L.inv();
+    const bool empty = ref == Q_EMPTY;
+    t0 = empty ? __int_as_float(0x7f800000) : max_(min_(f.x, n.x), max_(min_(f.y, n.y), min_(f.z, n.z)));
+    t1 = empty ? __int_as_float(0xff800000) : min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z)));
+  }
+  const bool ok = t1 >= t0 && t1 > 0.0f && (!cull || !(t0 > lim));
+  const float key = ok ? t0 : __int_as_float(0x7f800000);
+  const int rr = ok ? ref : Q_EMPTY;
+  float k[4] = {quad_bcast<0>(key), quad_bcast<1>(key), quad_bcast<2>(key), quad_bcast<3>(key)};
+  int r[4] = {quad_bcast<0>(rr), quad_bcast<1>(rr), quad_bcast<2>(rr), quad_bcast<3>(rr)};
+  return tl_qnode_push<false>(P, L, S, cull, k, r);
+}
+// triangle step: up to four triangles of the leaf at once; true when an any-hit ray is done
+RTD bool tl_tri_coop(const KParams& P, TraceLane& L, int c) {
+  const int n = min(4, L.tri_end - L.tri_i);
+  const int i = L.tri_i + c;
+  bool hit = false;
+  float dist = 0.0f, t = 0.0f;
+  if (c < n) {
+#ifdef RT_CHECK
+    if ((unsigned)i >= (unsigned)P.n_tri) printf("[rt check] coop triangle %d of %d\n", i, P.n_tri);
+#endif
+    const uint32_t o = (uint32_t)i * 48u;
+    hit = tl_tri_hit<true>(P, L, i, ld<float4>(P.trx, o), ld<float4>(P.trx, o + 16u), ld<float4>(P.trx, o + 32u), dist, t);
+  }
+  const int h = hit ? 1 : 0;
+  bool finished = false;
+  int used = n;
+  // triangle tri_i + q against the best after the ones before it (its hit flag: hit at <= the
+  // best before the step, which is >= the current best); one candidate broadcast at a time
+  auto merge = [&](int q, int hq, float dq, float tq) {
+    if (finished || !hq || dq > L.best) return;
+    const int iq = L.tri_i + q;
+    if (dq == L.best && !(L.besttri >= 0 && tie_wins(P, L, iq, L.besttri))) return;
+    L.best = dq;
+    L.besttri = iq;
+    L.bestt = tq;
+    if (L.anyhit) {
+      finished = true;
+      used = q + 1;
+    }
+  };
+  merge(0, quad_bcast<0>(h), quad_bcast<0>(dist), quad_bcast<0>(t));
+  merge(1, quad_bcast<1>(h), quad_bcast<1>(dist), quad_bcast<1>(t));
+  merge(2, quad_bcast<2>(h), quad_bcast<2>(dist), quad_bcast<2>(t));
+  merge(3, quad_bcast<3>(h), quad_bcast<3>(dist), quad_bcast<3>(t));
+  L.tri_i += used;
+  if (finished) L.tri_end = L.tri_i;
+  return finished;
+}
+// one cooperative dual step (tl_dual_calc's order); true when the ray is done
+RTD bool tl_coop_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull, int c) {
+  bool finished = false;
+  if (L.tri_i < L.tri_end) finished = tl_tri_coop(P, L, c);
+  bool needPop = false;
+  if (!finished && L.haveCur) {
+    if (ref_is_leaf(L.cur)) {
+      if (L.tri_i >= L.tri_end) {
+        L.tri_i = leaf_first(L.cur);
+        L.tri_end = L.tri_i + leaf_count(L.cur);
+        needPop = true;
+      }
+    } else {
+      needPop = tl_qnode_coop(P, L, TS, cull, c);
+    }
+  }
+  if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
+  return finished || (!L.haveCur && L.tri_i >= L.tri_end);
+}
+
+// Move a drained wave's live lanes (mask live, at most 16) to lane quads: lanes 4g..4g+3 take
+// the traversal state of the g-th live lane (registers by lane permutes; the LDS stack column and
+// its overflow entries entry by entry, every lane reading entry j of its source before any lane
+// writes entry j of its own).  Returns this lane's source (itself when its quad holds no ray).
+// Every lane of the wave must be active.
+RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, int lane) {
+  const int nl = __popcll(live);
+  const int g = lane >> 2;
+  unsigned long long m = live;
+  for (int j = 0; j < g && m; j++) m &= m - 1ull;
+  const int src = (g < nl && m) ? (int)__builtin_ctzll(m) : lane;
+  // (only the sources count: a lane that holds no ray may have no defined stack)
+  const int sp_src = __shfl(L.sp, src);
+  int spm = g < nl ? min(max(sp_src, 0), TS.KL + 64) : 0;
+  for (int o = 32; o > 0; o >>= 1) spm = max(spm, __shfl_xor(spm, o));
+  const uint32_t w0 = threadIdx.x & ~63u;
+  for (int j = 0; j < min(spm, TS.KL); j++) {
+    const int2 e = TS.lds0[j * TL_LANES + w0 + src];
+    TS.lds0[j * TL_LANES + w0 + lane] = e;
+  }
+  for (int j = TS.KL; j < spm; j++) {
+    const unsigned long long e = TS.ovf[(size_t)(j - TS.KL) * TS.ovs + w0 + src];
+    TS.ovf[(size_t)(j - TS.KL) * TS.ovs + w0 + lane] = e;
+  }
+  L.ox = __shfl(L.ox, src); L.oy = __shfl(L.oy, src); L.oz = __shfl(L.oz, src);
+  L.dx = __shfl(L.dx, src); L.dy = __shfl(L.dy, src); L.dz = __shfl(L.dz, src);
+  L.ix = __shfl(L.ix, src); L.iy = __shfl(L.iy, src); L.iz = __shfl(L.iz, src);
+  L.best = __shfl(L.best, src); L.bestt = __shfl(L.bestt, src); L.besttri = __shfl(L.besttri, src);
+  L.sp = sp_src; L.cur = __shfl(L.cur, src);
+  L.tri_i = __shfl(L.tri_i, src); L.tri_end = __shfl(L.tri_end, src);
+  L.offNx = __shfl(L.offNx, src); L.offNy = __shfl(L.offNy, src); L.offNz = __shfl(L.offNz, src);
+  L.offPk = (uint32_t)__shfl((int)L.offPk, src);
+  L.haveCur = __shfl((int)L.haveCur, src) != 0;
+  L.anyhit = __shfl((int)L.anyhit, src) != 0;
+  L.finite = __shfl((int)L.finite, src) != 0;
+  return src;
+}
+
 #ifndef RT_COST_PER_RAY  // tile-cost probe: node + triangle steps of a ray, plus this per ray (shade, queues)
 #define RT_COST_PER_RAY 16u
 #endif
@@ -864,6 +1033,10 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 #endif
 #ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed)
 #define RT_STATIC_FRAC 4
+#endif
+#ifndef RT_TRACE_COOP  // wf_trace (small passes, STATIC): a drained wave with at most this many rays left
+                       // moves them to four lanes each (0: off)
+#define RT_TRACE_COOP 0
 #endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
@@ -914,6 +1087,7 @@ void wf_trace(const WFParams W) {
   const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
 
   bool busy = false;
+  bool coop = false;  // RT_TRACE_COOP: four lanes per ray (wave-uniform)
   // per-wave pool of queue slots [pool_next, pool_end), refilled 64 at a time (wave-uniform)
   unsigned int pool_next = 0, pool_end = 0;
   const unsigned int tail_rays = gridDim.x * TL_LANES * RT_TAIL_FACTOR;
@@ -1010,6 +1184,19 @@ void wf_trace(const WFParams W) {
         pool_next += min((unsigned int)__popcll(idle), avail);
       }
     }
+    // a drained wave (queue and pool empty) with at most RT_TRACE_COOP rays left traces them with
+    // four lanes each (tl_coop_step, as in wf_finish): the pass ends on its longest rays
+    if (RT_TRACE_COOP && STATIC && WIDE && MODE == MODE_EXACT && !coop && drained && pool_next >= pool_end) {
+      const unsigned long long live = __ballot(busy);
+      const int nl = __popcll(live);
+      if (nl > 0 && nl <= RT_TRACE_COOP) {
+        coop = true;
+        const int src = coop_move(L, TS, live, lane);
+        const int e_src = __shfl(entry, src), b_src = __shfl((int)busy, src);
+        entry = e_src;
+        busy = (lane >> 2) < nl && b_src != 0;
+      }
+    }
     // (MODE_FAST: every ray the refill handed out may have been deferred, and the pool goes on:
     // the iteration then does nothing and the next one refills)
     if (!__any(busy) && (MODE != MODE_FAST || drained)) break;
@@ -1052,6 +1239,8 @@ void wf_trace(const WFParams W) {
       }
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
+    } else if (RT_TRACE_COOP && STATIC && WIDE && MODE == MODE_EXACT && coop) {
+      if (busy) finished = tl_coop_step(P, L, TS, cull, lane & 3);
     } else if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
@@ -1655,8 +1844,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // C3 1080p single frames -3.5% (32: -3.2%; two levels at 16 / 8 / 32: -2.8 / -2.5 / -2.1%)
 #define RT_FINISH_PRIO 16
 #endif
-#ifndef RT_FINISH_WPE  // 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2)
-#define RT_FINISH_WPE 2
+#ifndef RT_FINISH_COOP  // a drained wave with at most this many paths left (<= 16) moves to four lanes per
+// path (tl_coop_step; 0: off).  C3 1080p one-frame calls at 3 finisher waves/SIMD: 16 / 4 paths
+// -5.7 / -4.1% (the shade batch at 16 lanes), 16 with the shade batch at 64 lanes -6.6%
+// (profiles/r04_ab_single_coop_finisher_w3_C3.log)
+#define RT_FINISH_COOP 16
+#endif
+#ifndef RT_FINISH_COOP_SHADE_MIN  // the same in coop mode, in lanes (four per path): a wave of <= 16 paths
+// shades once all of them wait (or none traces)
+#define RT_FINISH_COOP_SHADE_MIN 64
+#endif
+#ifndef RT_FINISH_WPE  // at least 2 waves/SIMD (no spills): 1080p single frames 3.64 (4) / 3.50 (3) / 3.47 ms (2);
+// the compiler then kept the kernel at <= 168 VGPRs (3 waves); with the coop step it needs the
+// bound to stay there (2 waves: coop +3.6% instead of -6.6%)
+#define RT_FINISH_WPE 3
 #endif
 template <bool BSDF, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FINISH_WPE)))
@@ -1689,8 +1890,11 @@ void wf_finish(const WFParams W) {
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
+  bool coop = false;            // four lanes per path (RT_FINISH_COOP), wave-uniform
+  const int qc = lane & 3;      // this lane's share of its quad's path in coop mode
   TraceLane L;
   L.anyhit = false;
+  L.sp = 0;  // (defined for lanes that never hold a path: the coop move reads every lane's)
   // first queued ray of the path: the shadow ray (any-hit) if any, then the continuation, whose
   // 24 B are fetched together with the shadow ray's and held until it starts (no load in the
   // trace loop)
@@ -1740,6 +1944,24 @@ void wf_finish(const WFParams W) {
       }
       drained = base + want >= na;
     }
+#if RT_FINISH_COOP
+    if (WIDE && !coop && drained) {
+      const unsigned long long live = __ballot(st != FS_IDLE);
+      const int nl = __popcll(live);
+      if (nl > 0 && nl <= RT_FINISH_COOP) {
+        // the g-th live lane's path moves to lanes 4g .. 4g+3
+        coop = true;
+        const int g = lane >> 2;
+        const int src = coop_move(L, TS, live, lane);
+        path = __shfl(path, src);
+        contNext = __shfl((int)contNext, src) != 0;
+        ca.x = __shfl(ca.x, src); ca.y = __shfl(ca.y, src); ca.z = __shfl(ca.z, src); ca.w = __shfl(ca.w, src);
+        cb.x = __shfl(cb.x, src); cb.y = __shfl(cb.y, src);
+        const int st_src = __shfl(st, src);  // (outside the select: a lane-permute from a lane masked off reads 0)
+        st = g < nl ? st_src : (int)FS_IDLE;
+      }
+    }
+#endif
     if (!__any(st != FS_IDLE)) break;
     {  // fuller waves issue first (s_setprio by the lanes holding a path; see RT_FINISH_PRIO)
       const int busy = __popcll(__ballot(st != FS_IDLE));
@@ -1752,7 +1974,7 @@ void wf_finish(const WFParams W) {
     // for the wave's slowest ray of every bounce, only for a batch of shade steps
     while (true) {
       const unsigned long long tr = __ballot(st == FS_TRACE);
-      if (!tr || __popcll(__ballot(st == FS_SHADE)) >= RT_FINISH_SHADE_MIN) break;
+      if (!tr || __popcll(__ballot(st == FS_SHADE)) >= (coop ? RT_FINISH_COOP_SHADE_MIN : RT_FINISH_SHADE_MIN)) break;
 #ifdef RT_FINISH_PROF
       prof_it++;
       if (drained) {
@@ -1762,9 +1984,10 @@ void wf_finish(const WFParams W) {
           if (!prof_at[q] && busy <= lim[q]) { prof_at[q] = wall_clock64(); prof_it_at[q] = prof_it; }
       }
 #endif
-      if (st == FS_TRACE && (!P.has_scene || tl_step_prefetch<WIDE>(P, L, TS, cull))) {
+      if (st == FS_TRACE && (!P.has_scene || (RT_FINISH_COOP && WIDE && coop ? tl_coop_step(P, L, TS, cull, qc)
+                                                                             : tl_step_prefetch<WIDE>(P, L, TS, cull)))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
-        nrays++;
+        if (!coop || qc == 0) nrays++;
         if (contNext) begin_cont();
         else st = FS_SHADE;
       }
@@ -1785,12 +2008,15 @@ void wf_finish(const WFParams W) {
       const WFParams* Wl = (const WFParams*)Wk;
       const KParams& PL = Wl->K;
       const Env EL{PL.hdr, PL.cache, PL.light, PL.hdr_w, PL.hdr_h, PL.hdr_res, PL.env_angle, PL.env_intensity};
-      const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, nsamples);
+      unsigned long long ns = 0;  // (a coop quad runs its path's shade step on all four lanes: counted once)
+      const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, ns);
 #else
-      const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, nsamples);
+      unsigned long long ns = 0;
+      const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, ns);
 #endif
+      if (!coop || qc == 0) nsamples += ns;
       if (sh) {
-        nsteps++;
+        if (!coop || qc == 0) nsteps++;
         if (o.qShadow || o.qCont) {
           st = FS_TRACE;
           begin_rays(o.qShadow, o.qCont);

@@ -19,7 +19,7 @@ for v in variants:
         for r in csv.DictReader(open(f)):
             dur[kname(r)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
     cnt = defaultdict(lambda: defaultdict(float))
-    for p in ("a", "b"):
+    for p in ("a", "b", "c"):
         for f in set(glob.glob(f"{root}/{v}/{p}/**/run_counter_collection.csv", recursive=True) +
                      glob.glob(f"{root}/{v}/{p}/run_counter_collection.csv")):
             for r in csv.DictReader(open(f)):
@@ -47,6 +47,10 @@ for v in variants:
             if rays and k == "wf_trace":
                 line += (f"  per ray: valu {c['SQ_INSTS_VALU'] / rays:.1f} salu {c.get('SQ_INSTS_SALU', 0) / rays:.1f}"
                          f"  salu/valu {c.get('SQ_INSTS_SALU', 0) / c['SQ_INSTS_VALU']:.2f}")
+        if c.get("WRITE_SIZE"):  # KB (MI355X_MICROARCH.md)
+            line += f"  write {c['WRITE_SIZE'] * 1024 / 1e9:.2f} GB"
+            if rays and k == "wf_trace":
+                line += f" ({c['WRITE_SIZE'] * 1024 / rays:.1f} B written per ray)"
         if c.get("TCC_HIT_sum"):
             line += f"  L2hit {c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']):.3f}"
         print(line)
