@@ -72,3 +72,13 @@ def test_stats_struct_matches_header(tmp_path):
     assert ver == renderer.RT_ABI_VERSION
     lib = C.CDLL(str(ROOT / "opengl-ray-tracing-framework_amd" / "lib" / "librtamd.so"))
     assert lib.rt_abi_version() == ver
+
+
+def test_flag_constants_match_header():
+    """Every RT_FLAG_* of include/rt_abi.h has the same value in the ctypes binding (and no
+    binding flag is missing from the header)."""
+    text = (ROOT / "include" / "rt_abi.h").read_text()
+    header = {k: int(v) for k, v in re.findall(r"^\s*(RT_FLAG_\w+)\s*=\s*(\d+)", text, re.M)}
+    binding = {k: getattr(renderer, k) for k in dir(renderer) if k.startswith("RT_FLAG_")}
+    assert len(header) >= 7
+    assert header == binding
