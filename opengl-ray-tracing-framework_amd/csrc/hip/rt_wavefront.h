@@ -883,22 +883,21 @@ RTD bool tl_step_prefetch(const KParams& P, TraceLane& L, const TraceStack& TS, 
 // and merges the four triangle candidates in index order with the sequential rules (dist <= best,
 // exact ties by tie_wins, an any-hit ray stops at its first accepted triangle): the same closest
 // hit as testing them one after the other.
-template <int K>
-RTD int quad_bcast(int x) {  // lane K of each quad, to all four
-  return __builtin_amdgcn_update_dpp(0, x, K | K << 2 | K << 4 | K << 6, 0xf, 0xf, false);
+// lane K of each group of G (2 or 4) consecutive lanes, to the whole group (DPP quad_perm)
+template <int G, int K>
+RTD int grp_bcast(int x) {
+  constexpr int a = K, b = (G == 4) ? K : K + 2;
+  return __builtin_amdgcn_update_dpp(0, x, a | a << 2 | b << 4 | b << 6, 0xf, 0xf, false);
 }
-template <int K>
-RTD float quad_bcast(float x) {
-  return __int_as_float(quad_bcast<K>(__float_as_int(x)));
+template <int G, int K>
+RTD float grp_bcast(float x) {
+  return __int_as_float(grp_bcast<G, K>(__float_as_int(x)));
 }
-// node step: child c's box with the operations of tl_qnode_keys, then every lane pushes all four
-RTD bool tl_qnode_coop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, int c) {
-  const uint32_t off = ((uint32_t)L.cur << 7) + 4u * (uint32_t)c;
-#ifdef RT_CHECK
-  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) printf("[rt check] coop node %d of %d\n", L.cur, P.n_qnodes);
-#endif
+// child j's box of node L.cur with the operations of tl_qnode_keys: its sort key and ref (+inf /
+// Q_EMPTY when missed or culled)
+RTD void coop_box(const KParams& P, const TraceLane& L, int j, bool cull, float lim, float& key, int& rr) {
+  const uint32_t off = ((uint32_t)L.cur << 7) + 4u * (uint32_t)j;
   const int ref = ld<int>(P.qnodes, off + 96u);
-  const float lim = cull ? L.limit(P.cull_eps) : __int_as_float(0x7f800000);
   float t0, t1;
   if (L.finite) {  // tl_qnode_t01 for one child
     const float nx = ld<float>(P.qnodes, off + L.offNx), ny = ld<float>(P.qnodes, off + L.offNy),
@@ -915,15 +914,38 @@ RTD bool tl_qnode_coop(const KParams& P, TraceLane& L, const TraceStack& S, bool
     t1 = empty ? __int_as_float(0xff800000) : min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z)));
   }
   const bool ok = t1 >= t0 && t1 > 0.0f && (!cull || !(t0 > lim));
-  const float key = ok ? t0 : __int_as_float(0x7f800000);
-  const int rr = ok ? ref : Q_EMPTY;
-  float k[4] = {quad_bcast<0>(key), quad_bcast<1>(key), quad_bcast<2>(key), quad_bcast<3>(key)};
-  int r[4] = {quad_bcast<0>(rr), quad_bcast<1>(rr), quad_bcast<2>(rr), quad_bcast<3>(rr)};
+  key = ok ? t0 : __int_as_float(0x7f800000);
+  rr = ok ? ref : Q_EMPTY;
+}
+// node step: lane c of the group tests children c (and c + 2 for pairs), then every lane pushes
+// all four
+template <int G>
+RTD bool tl_qnode_coop(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, int c) {
+#ifdef RT_CHECK
+  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) printf("[rt check] coop node %d of %d\n", L.cur, P.n_qnodes);
+#endif
+  const float lim = cull ? L.limit(P.cull_eps) : __int_as_float(0x7f800000);
+  float ka, k[4];
+  int ra, r[4];
+  coop_box(P, L, c, cull, lim, ka, ra);
+  k[0] = grp_bcast<G, 0>(ka); k[1] = grp_bcast<G, 1>(ka);
+  r[0] = grp_bcast<G, 0>(ra); r[1] = grp_bcast<G, 1>(ra);
+  if (G == 4) {
+    k[2] = grp_bcast<G, 2>(ka); k[3] = grp_bcast<G, 3>(ka);
+    r[2] = grp_bcast<G, 2>(ra); r[3] = grp_bcast<G, 3>(ra);
+  } else {
+    float kb;
+    int rb;
+    coop_box(P, L, c + 2, cull, lim, kb, rb);
+    k[2] = grp_bcast<G, 0>(kb); k[3] = grp_bcast<G, 1>(kb);
+    r[2] = grp_bcast<G, 0>(rb); r[3] = grp_bcast<G, 1>(rb);
+  }
   return tl_qnode_push<false>(P, L, S, cull, k, r);
 }
-// triangle step: up to four triangles of the leaf at once; true when an any-hit ray is done
+// triangle step: up to G triangles of the leaf at once; true when an any-hit ray is done
+template <int G>
 RTD bool tl_tri_coop(const KParams& P, TraceLane& L, int c) {
-  const int n = min(4, L.tri_end - L.tri_i);
+  const int n = min(G, L.tri_end - L.tri_i);
   const int i = L.tri_i + c;
   bool hit = false;
   float dist = 0.0f, t = 0.0f;
@@ -951,18 +973,21 @@ RTD bool tl_tri_coop(const KParams& P, TraceLane& L, int c) {
       used = q + 1;
     }
   };
-  merge(0, quad_bcast<0>(h), quad_bcast<0>(dist), quad_bcast<0>(t));
-  merge(1, quad_bcast<1>(h), quad_bcast<1>(dist), quad_bcast<1>(t));
-  merge(2, quad_bcast<2>(h), quad_bcast<2>(dist), quad_bcast<2>(t));
-  merge(3, quad_bcast<3>(h), quad_bcast<3>(dist), quad_bcast<3>(t));
+  merge(0, grp_bcast<G, 0>(h), grp_bcast<G, 0>(dist), grp_bcast<G, 0>(t));
+  merge(1, grp_bcast<G, 1>(h), grp_bcast<G, 1>(dist), grp_bcast<G, 1>(t));
+  if (G == 4) {
+    merge(2, grp_bcast<G, 2>(h), grp_bcast<G, 2>(dist), grp_bcast<G, 2>(t));
+    merge(3, grp_bcast<G, 3>(h), grp_bcast<G, 3>(dist), grp_bcast<G, 3>(t));
+  }
   L.tri_i += used;
   if (finished) L.tri_end = L.tri_i;
   return finished;
 }
 // one cooperative dual step (tl_dual_calc's order); true when the ray is done
+template <int G>
 RTD bool tl_coop_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull, int c) {
   bool finished = false;
-  if (L.tri_i < L.tri_end) finished = tl_tri_coop(P, L, c);
+  if (L.tri_i < L.tri_end) finished = tl_tri_coop<G>(P, L, c);
   bool needPop = false;
   if (!finished && L.haveCur) {
     if (ref_is_leaf(L.cur)) {
@@ -972,21 +997,22 @@ RTD bool tl_coop_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool
         needPop = true;
       }
     } else {
-      needPop = tl_qnode_coop(P, L, TS, cull, c);
+      needPop = tl_qnode_coop<G>(P, L, TS, cull, c);
     }
   }
   if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
   return finished || (!L.haveCur && L.tri_i >= L.tri_end);
 }
 
-// Move a drained wave's live lanes (mask live, at most 16) to lane quads: lanes 4g..4g+3 take
-// the traversal state of the g-th live lane (registers by lane permutes; the LDS stack column and
+// Move a drained wave's live lanes (mask live, at most 64 / G) to lane groups of G: lanes
+// G*g .. G*g+G-1 take the traversal state of the g-th live lane (registers by lane permutes; the LDS stack column and
 // its overflow entries entry by entry, every lane reading entry j of its source before any lane
-// writes entry j of its own).  Returns this lane's source (itself when its quad holds no ray).
+// writes entry j of its own).  Returns this lane's source (itself when its group holds no ray).
 // Every lane of the wave must be active.
+template <int G>
 RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, int lane) {
   const int nl = __popcll(live);
-  const int g = lane >> 2;
+  const int g = lane / G;
   unsigned long long m = live;
   for (int j = 0; j < g && m; j++) m &= m - 1ull;
   const int src = (g < nl && m) ? (int)__builtin_ctzll(m) : lane;
@@ -1191,7 +1217,7 @@ void wf_trace(const WFParams W) {
       const int nl = __popcll(live);
       if (nl > 0 && nl <= RT_TRACE_COOP) {
         coop = true;
-        const int src = coop_move(L, TS, live, lane);
+        const int src = coop_move<4>(L, TS, live, lane);
         const int e_src = __shfl(entry, src), b_src = __shfl((int)busy, src);
         entry = e_src;
         busy = (lane >> 2) < nl && b_src != 0;
@@ -1240,7 +1266,7 @@ void wf_trace(const WFParams W) {
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
     } else if (RT_TRACE_COOP && STATIC && WIDE && MODE == MODE_EXACT && coop) {
-      if (busy) finished = tl_coop_step(P, L, TS, cull, lane & 3);
+      if (busy) finished = tl_coop_step<4>(P, L, TS, cull, lane & 3);
     } else if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
@@ -1850,6 +1876,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // (profiles/r04_ab_single_coop_finisher_w3_C3.log)
 #define RT_FINISH_COOP 16
 #endif
+#ifndef RT_FINISH_COOP2  // ... and with at most this many (<= 32), two lanes per path until 16 are left (0: off)
+#define RT_FINISH_COOP2 0
+#endif
 #ifndef RT_FINISH_COOP_SHADE_MIN  // the same in coop mode, in lanes (four per path): a wave of <= 16 paths
 // shades once all of them wait (or none traces)
 #define RT_FINISH_COOP_SHADE_MIN 64
@@ -1890,8 +1919,8 @@ void wf_finish(const WFParams W) {
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
-  bool coop = false;            // four lanes per path (RT_FINISH_COOP), wave-uniform
-  const int qc = lane & 3;      // this lane's share of its quad's path in coop mode
+  int coop = 0;  // lanes per path: 0 (one), 2 (RT_FINISH_COOP2) or 4 (RT_FINISH_COOP); wave-uniform
+  auto lead = [&]() { return coop == 0 || (lane & (coop - 1)) == 0; };  // counts for its group
   TraceLane L;
   L.anyhit = false;
   L.sp = 0;  // (defined for lanes that never hold a path: the coop move reads every lane's)
@@ -1945,14 +1974,16 @@ void wf_finish(const WFParams W) {
       drained = base + want >= na;
     }
 #if RT_FINISH_COOP
-    if (WIDE && !coop && drained) {
-      const unsigned long long live = __ballot(st != FS_IDLE);
+    if (WIDE && coop < 4 && drained) {
+      // paths left: one per lane, or one per group of the current coop mode
+      const unsigned long long live = __ballot(st != FS_IDLE && lead());
       const int nl = __popcll(live);
-      if (nl > 0 && nl <= RT_FINISH_COOP) {
-        // the g-th live lane's path moves to lanes 4g .. 4g+3
-        coop = true;
-        const int g = lane >> 2;
-        const int src = coop_move(L, TS, live, lane);
+      const int G = nl <= RT_FINISH_COOP ? 4 : (coop == 0 && nl <= RT_FINISH_COOP2) ? 2 : 0;
+      if (nl > 0 && G > coop) {
+        // the g-th path moves to lanes G*g .. G*g+G-1
+        const int src = G == 4 ? coop_move<4>(L, TS, live, lane) : coop_move<2>(L, TS, live, lane);
+        const int g = lane / G;
+        coop = G;
         path = __shfl(path, src);
         contNext = __shfl((int)contNext, src) != 0;
         ca.x = __shfl(ca.x, src); ca.y = __shfl(ca.y, src); ca.z = __shfl(ca.z, src); ca.w = __shfl(ca.w, src);
@@ -1984,10 +2015,12 @@ void wf_finish(const WFParams W) {
           if (!prof_at[q] && busy <= lim[q]) { prof_at[q] = wall_clock64(); prof_it_at[q] = prof_it; }
       }
 #endif
-      if (st == FS_TRACE && (!P.has_scene || (RT_FINISH_COOP && WIDE && coop ? tl_coop_step(P, L, TS, cull, qc)
-                                                                             : tl_step_prefetch<WIDE>(P, L, TS, cull)))) {
+      if (st == FS_TRACE &&
+          (!P.has_scene || (RT_FINISH_COOP && WIDE && coop == 4   ? tl_coop_step<4>(P, L, TS, cull, lane & 3)
+                            : RT_FINISH_COOP && WIDE && coop == 2 ? tl_coop_step<2>(P, L, TS, cull, lane & 1)
+                                                                  : tl_step_prefetch<WIDE>(P, L, TS, cull)))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
-        if (!coop || qc == 0) nrays++;
+        if (lead()) nrays++;
         if (contNext) begin_cont();
         else st = FS_SHADE;
       }
@@ -2008,15 +2041,15 @@ void wf_finish(const WFParams W) {
       const WFParams* Wl = (const WFParams*)Wk;
       const KParams& PL = Wl->K;
       const Env EL{PL.hdr, PL.cache, PL.light, PL.hdr_w, PL.hdr_h, PL.hdr_res, PL.env_angle, PL.env_intensity};
-      unsigned long long ns = 0;  // (a coop quad runs its path's shade step on all four lanes: counted once)
+      unsigned long long ns = 0;  // (a coop group runs its path's shade step on all its lanes: counted once)
       const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, ns);
 #else
       unsigned long long ns = 0;
       const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, ns);
 #endif
-      if (!coop || qc == 0) nsamples += ns;
+      if (lead()) nsamples += ns;
       if (sh) {
-        if (!coop || qc == 0) nsteps++;
+        if (lead()) nsteps++;
         if (o.qShadow || o.qCont) {
           st = FS_TRACE;
           begin_rays(o.qShadow, o.qCont);
