@@ -1061,8 +1061,14 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 #define RT_STATIC_FRAC 4
 #endif
 #ifndef RT_TRACE_COOP  // wf_trace (small passes, STATIC): a drained wave with at most this many rays left
-                       // moves them to four lanes each (0: off)
-#define RT_TRACE_COOP 0
+                       // moves them to four lanes each (0: off).  C3 1080p one-frame calls, with the
+                       // finisher's quads: -12.7% back-to-back / -8.6% synchronised against the
+                       // build without either, vs -7.6% / -1.3% for the finisher's alone; lane pairs
+                       // from 32 paths in the finisher cost 2-3% (profiles/r04_ab_single_coop_trace_tails_pairs_C3.log)
+#define RT_TRACE_COOP 16
+#endif
+#ifndef RT_TRACE_COOP_BULK  // the same in the large passes' kernels (1: on)
+#define RT_TRACE_COOP_BULK 0
 #endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
@@ -1212,7 +1218,8 @@ void wf_trace(const WFParams W) {
     }
     // a drained wave (queue and pool empty) with at most RT_TRACE_COOP rays left traces them with
     // four lanes each (tl_coop_step, as in wf_finish): the pass ends on its longest rays
-    if (RT_TRACE_COOP && STATIC && WIDE && MODE == MODE_EXACT && !coop && drained && pool_next >= pool_end) {
+    if (RT_TRACE_COOP && (STATIC || (RT_TRACE_COOP_BULK && !COUNT)) && WIDE && MODE == MODE_EXACT && !coop && drained &&
+        pool_next >= pool_end) {
       const unsigned long long live = __ballot(busy);
       const int nl = __popcll(live);
       if (nl > 0 && nl <= RT_TRACE_COOP) {
@@ -1265,7 +1272,7 @@ void wf_trace(const WFParams W) {
       }
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
-    } else if (RT_TRACE_COOP && STATIC && WIDE && MODE == MODE_EXACT && coop) {
+    } else if (RT_TRACE_COOP && (STATIC || (RT_TRACE_COOP_BULK && !COUNT)) && WIDE && MODE == MODE_EXACT && coop) {
       if (busy) finished = tl_coop_step<4>(P, L, TS, cull, lane & 3);
     } else if (busy) {
       if (L.tri_i < L.tri_end) {
