@@ -195,3 +195,21 @@ def test_path_persistent_finisher_matches_oracle(gpu_renderer, env_maps, name, f
         gpu_renderer.set_finish(2, 8 << 20)
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("name", ["C3", "C4"])
+def test_lane_quads_move_overflow_stacks(gpu_dev_renderer, env_maps, monkeypatch, name):
+    """The lane-quad tails (wf_finish and the small passes' wf_trace) copy each path's
+    stack to its quad, LDS entries and overflow entries alike.  With one LDS entry per lane
+    (RT_LDS_STACK=1, dev library) nearly every stacked subtree is in the overflow columns when a
+    wave moves its paths, and the image and the ray count still equal the oracle's."""
+    from rtamd.renderer import RT_FLAG_FINISH
+    sd = cf.config_scene(name)
+    W, H = 80, 48
+    fp = cf.frame_params(W, H, flags=RT_FLAG_FINISH)
+    ro, frames = frames_for(fp, 1, 1)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    monkeypatch.setenv("RT_LDS_STACK", "1")
+    img, st = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
