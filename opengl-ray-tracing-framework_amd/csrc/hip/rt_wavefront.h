@@ -1070,6 +1070,11 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 #ifndef RT_TRACE_COOP_BULK  // the same in the large passes' kernels (1: on)
 #define RT_TRACE_COOP_BULK 0
 #endif
+#ifndef RT_RES_NT  // wf_trace writes its results with non-temporal stores (1): C3 bulk +0.45%
+                   // (profiles/r04_ab_bulk_result_nt_C3.log); its HBM writes stay ~30 B per ray
+                   // (scattered 4-B results and 8-B overflow-stack entries, each a partial sector)
+#define RT_RES_NT 1
+#endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
 #endif
@@ -1313,7 +1318,8 @@ void wf_trace(const WFParams W) {
       busy = false;
     }
     if (busy && finished) {
-      S.res[entry] = L.besttri;
+      if (RT_RES_NT) __builtin_nontemporal_store(L.besttri, &S.res[entry]);
+      else S.res[entry] = L.besttri;
       if (COUNT) {
         if (P.tile_cost) {  // rt_tile_costs probe: traversal steps + a per-ray share for the shade
           const unsigned int w = (unsigned int)(entry >> 1) / (unsigned int)P.n_frames;
