@@ -92,9 +92,54 @@ RTD void p1_ray(const WFState& S, unsigned int n_frames, unsigned int path, cons
     ox = o.x + c.x * a.w; oy = o.y + c.y * a.w; oz = o.z + c.z * a.w;
   }
 }
+// path-state and ray stores of the shade step: non-temporal with RT_SHADE_NT (rows written once
+// per pass and read by the next pass's kernels, after they have left the caches)
+#ifndef RT_SHADE_NT  // C3 bulk +1.13%, one-frame calls +0.3% (noise) (profiles/r04_ab_nt_shade_stores_C3.log)
+#define RT_SHADE_NT 1
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef float nt_f2 __attribute__((ext_vector_type(2)));
+typedef unsigned int nt_u2 __attribute__((ext_vector_type(2)));
+RTD void st_row(float4* p, float4 v) {
+  if (RT_SHADE_NT) __builtin_nontemporal_store(nt_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_f4*>(p));
+  else *p = v;
+}
+RTD void st_row(float2* p, float2 v) {
+  if (RT_SHADE_NT) __builtin_nontemporal_store(nt_f2{v.x, v.y}, reinterpret_cast<nt_f2*>(p));
+  else *p = v;
+}
+RTD void st_row(uint2* p, uint2 v) {
+  if (RT_SHADE_NT) __builtin_nontemporal_store(nt_u2{v.x, v.y}, reinterpret_cast<nt_u2*>(p));
+  else *p = v;
+}
+// rows read once per pass (rays by the trace, path state by the shade): non-temporal loads with
+// RT_TRACE_NTL / RT_SHADE_NTL, so they do not displace scene data in the caches
+#ifndef RT_TRACE_NTL
+#define RT_TRACE_NTL 0
+#endif
+#ifndef RT_SHADE_NTL
+#define RT_SHADE_NTL 0
+#endif
+template <bool NT>
+RTD float4 ld_row(const float4* p) {
+  if (!NT) return *p;
+  const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+RTD float2 ld_row(const float2* p) {
+  if (!NT) return *p;
+  const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p));
+  return make_float2(v.x, v.y);
+}
+template <bool NT>
+RTD int ld_row(const int* p) {
+  if (!NT) return *p;
+  return __builtin_nontemporal_load(p);
+}
 RTD void put_ray(float4* a, float2* b, unsigned int p, float ox, float oy, float oz, float dx, float dy, float dz) {
-  a[p] = make_float4(ox, oy, oz, dx);
-  b[p] = make_float2(dy, dz);
+  st_row(a + p, make_float4(ox, oy, oz, dx));
+  st_row(b + p, make_float2(dy, dz));
 }
 
 struct WFParams {
@@ -1198,15 +1243,15 @@ void wf_trace(const WFParams W) {
             L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
             L.dx = d.x; L.dy = d.y; L.dz = d.z;
           } else {
-            entry = MODE == MODE_SLOWIN ? slow_list[qi] : S.queue[qin][qi];
+            entry = MODE == MODE_SLOWIN ? slow_list[qi] : ld_row<RT_TRACE_NTL>(S.queue[qin] + qi);
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
-            const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
+            const float4 oa = ld_row<RT_TRACE_NTL>((L.anyhit ? S.sa : S.ra) + path);
             if (P1) {  // 16-B rays from pass 0
               p1_ray(S, (unsigned)W.n_frames, (unsigned)path, oa, L.ox, L.oy, L.oz);
               L.dx = oa.x; L.dy = oa.y; L.dz = oa.z;
             } else {
-              const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
+              const float2 ob = ld_row<RT_TRACE_NTL>((L.anyhit ? S.sb : S.rb) + path);
               L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
               L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
             }
@@ -1439,15 +1484,15 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     // uniform test), so no load waits for the flags; the flags still decide what is used
     int rsh = 0;
     if (loadPrev) {
-      a0 = S.s0[path]; a2 = S.s2[path];
+      a0 = ld_row<RT_SHADE_NTL>(S.s0 + path); a2 = ld_row<RT_SHADE_NTL>(S.s2 + path);
       rsh = S.res[2 * path + 1];
       // (PF_ZLO) a path whose Lo and Le0 are +0 (every path after a non-emissive camera hit, whose
       // NEE is still pending) skips the s1 row and, without a shadow ray, the s3 row
       if (!(a5.z & PF_ZLO)) {
-        a1 = S.s1[path];
-        a3 = S.s3[path];
+        a1 = ld_row<RT_SHADE_NTL>(S.s1 + path);
+        a3 = ld_row<RT_SHADE_NTL>(S.s3 + path);
       } else if (a5.z & PF_SHADOW) {
-        a3 = S.s3[path];
+        a3 = ld_row<RT_SHADE_NTL>(S.s3 + path);
       }
     }
     const int rc0 = S.res[2 * path];
@@ -1462,8 +1507,8 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       oo0 = make_float4(ox, oy, oz, 0.0f);
       dd0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
     } else {
-      const float4 ra0 = S.ra[path];
-      const float2 rb0 = S.rb[path];
+      const float4 ra0 = ld_row<RT_SHADE_NTL>(S.ra + path);
+      const float2 rb0 = ld_row<RT_SHADE_NTL>(S.rb + path);
       oo0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
       dd0 = make_float4(ra0.w, rb0.x, rb0.y, 0.0f);
     }
@@ -1715,7 +1760,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       const f3 acc = bw.x * fin + bw.y * mk3(h.x, h.y, h.z);
       P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
     } else {
-      S.fin[path] = make_float4(fin.x, fin.y, fin.z, 0.0f);
+      st_row(S.fin + path, make_float4(fin.x, fin.y, fin.z, 0.0f));
     }
     nsamples++;
   }
@@ -1726,16 +1771,16 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     const bool zlo = (__float_as_uint(Lo.x) | __float_as_uint(Lo.y) | __float_as_uint(Lo.z) |
                                 __float_as_uint(Le0.x) | __float_as_uint(Le0.y) | __float_as_uint(Le0.z)) == 0u;
     if (zlo) nflags |= PF_ZLO;
-    S.s0[path] = make_float4(hist.x, hist.y, hist.z, evp);
-    if (!zlo) S.s1[path] = make_float4(Lo.x, Lo.y, Lo.z, Le0.x);
-    S.s2[path] = make_float4(evf.x, evf.y, evf.z, Le0.y);
-    if (!zlo || qShadow) S.s3[path] = make_float4(cnee.x, cnee.y, cnee.z, Le0.z);
-    if (nflags & PF_CMED) S.s4[path] = make_float4(cmed.x, cmed.y, cmed.z, 0.0f);
-    if (!BSDF && qCont) S.s4[path] = make_float4(bNdotL, 0.0f, 0.0f, 0.0f);
-    S.s5[path] = make_uint2(wseed, bounce << 8 | nflags);
+    st_row(S.s0 + path, make_float4(hist.x, hist.y, hist.z, evp));
+    if (!zlo) st_row(S.s1 + path, make_float4(Lo.x, Lo.y, Lo.z, Le0.x));
+    st_row(S.s2 + path, make_float4(evf.x, evf.y, evf.z, Le0.y));
+    if (!zlo || qShadow) st_row(S.s3 + path, make_float4(cnee.x, cnee.y, cnee.z, Le0.z));
+    if (nflags & PF_CMED) st_row(S.s4 + path, make_float4(cmed.x, cmed.y, cmed.z, 0.0f));
+    if (!BSDF && qCont) st_row(S.s4 + path, make_float4(bNdotL, 0.0f, 0.0f, 0.0f));
+    st_row(S.s5 + path, make_uint2(wseed, bounce << 8 | nflags));
     if (camPass && W.p1_compact) {  // (uniform) 16-B rays from the pixel's camera hit point
-      if (qCont) S.ra[path] = make_float4(contD.x, contD.y, contD.z, contS);
-      if (qShadow) S.sa[path] = make_float4(shD.x, shD.y, shD.z, 0.0f);
+      if (qCont) st_row(S.ra + path, make_float4(contD.x, contD.y, contD.z, contS));
+      if (qShadow) st_row(S.sa + path, make_float4(shD.x, shD.y, shD.z, 0.0f));
     } else {
       if (qCont) put_ray(S.ra, S.rb, path, contO.x, contO.y, contO.z, contD.x, contD.y, contD.z);
       if (qShadow) put_ray(S.sa, S.sb, path, shO.x, shO.y, shO.z, shD.x, shD.y, shD.z);
