@@ -112,31 +112,6 @@ RTD void st_row(uint2* p, uint2 v) {
   if (RT_SHADE_NT) __builtin_nontemporal_store(nt_u2{v.x, v.y}, reinterpret_cast<nt_u2*>(p));
   else *p = v;
 }
-// rows read once per pass (rays by the trace, path state by the shade): non-temporal loads with
-// RT_TRACE_NTL / RT_SHADE_NTL, so they do not displace scene data in the caches
-#ifndef RT_TRACE_NTL
-#define RT_TRACE_NTL 0
-#endif
-#ifndef RT_SHADE_NTL
-#define RT_SHADE_NTL 0
-#endif
-template <bool NT>
-RTD float4 ld_row(const float4* p) {
-  if (!NT) return *p;
-  const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-template <bool NT>
-RTD float2 ld_row(const float2* p) {
-  if (!NT) return *p;
-  const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p));
-  return make_float2(v.x, v.y);
-}
-template <bool NT>
-RTD int ld_row(const int* p) {
-  if (!NT) return *p;
-  return __builtin_nontemporal_load(p);
-}
 RTD void put_ray(float4* a, float2* b, unsigned int p, float ox, float oy, float oz, float dx, float dy, float dz) {
   st_row(a + p, make_float4(ox, oy, oz, dx));
   st_row(b + p, make_float2(dy, dz));
@@ -1243,15 +1218,15 @@ void wf_trace(const WFParams W) {
             L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
             L.dx = d.x; L.dy = d.y; L.dz = d.z;
           } else {
-            entry = MODE == MODE_SLOWIN ? slow_list[qi] : ld_row<RT_TRACE_NTL>(S.queue[qin] + qi);
+            entry = MODE == MODE_SLOWIN ? slow_list[qi] : S.queue[qin][qi];
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
-            const float4 oa = ld_row<RT_TRACE_NTL>((L.anyhit ? S.sa : S.ra) + path);
+            const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
             if (P1) {  // 16-B rays from pass 0
               p1_ray(S, (unsigned)W.n_frames, (unsigned)path, oa, L.ox, L.oy, L.oz);
               L.dx = oa.x; L.dy = oa.y; L.dz = oa.z;
             } else {
-              const float2 ob = ld_row<RT_TRACE_NTL>((L.anyhit ? S.sb : S.rb) + path);
+              const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
               L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
               L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
             }
@@ -1484,15 +1459,15 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     // uniform test), so no load waits for the flags; the flags still decide what is used
     int rsh = 0;
     if (loadPrev) {
-      a0 = ld_row<RT_SHADE_NTL>(S.s0 + path); a2 = ld_row<RT_SHADE_NTL>(S.s2 + path);
+      a0 = S.s0[path]; a2 = S.s2[path];
       rsh = S.res[2 * path + 1];
       // (PF_ZLO) a path whose Lo and Le0 are +0 (every path after a non-emissive camera hit, whose
       // NEE is still pending) skips the s1 row and, without a shadow ray, the s3 row
       if (!(a5.z & PF_ZLO)) {
-        a1 = ld_row<RT_SHADE_NTL>(S.s1 + path);
-        a3 = ld_row<RT_SHADE_NTL>(S.s3 + path);
+        a1 = S.s1[path];
+        a3 = S.s3[path];
       } else if (a5.z & PF_SHADOW) {
-        a3 = ld_row<RT_SHADE_NTL>(S.s3 + path);
+        a3 = S.s3[path];
       }
     }
     const int rc0 = S.res[2 * path];
@@ -1507,8 +1482,8 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       oo0 = make_float4(ox, oy, oz, 0.0f);
       dd0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
     } else {
-      const float4 ra0 = ld_row<RT_SHADE_NTL>(S.ra + path);
-      const float2 rb0 = ld_row<RT_SHADE_NTL>(S.rb + path);
+      const float4 ra0 = S.ra[path];
+      const float2 rb0 = S.rb[path];
       oo0 = make_float4(ra0.x, ra0.y, ra0.z, 0.0f);
       dd0 = make_float4(ra0.w, rb0.x, rb0.y, 0.0f);
     }
