@@ -35,12 +35,18 @@
 #include <stddef.h>
 #include <stdint.h>
 
-/* ABI version of this header.  4: rt_stats gained pass0_steps, pass1_steps, finish_steps and
- * trace_busy_ms (round 4; round 3 had added path_steps and p1_rays), and rt_stats_get_sized /
- * rt_abi_version / RT_FLAG_SERIAL appeared.  A binding built against an
- * older header calls rt_stats_get_sized with its own sizeof(rt_stats), or checks rt_abi_version()
- * at load time. */
-#define RT_ABI_VERSION 4
+/* ABI version of this header.
+ * 4: rt_stats gained pass0_steps, pass1_steps, finish_steps and trace_busy_ms (round 4; round 3
+ *    had added path_steps and p1_rays), and rt_stats_get_sized / rt_abi_version / RT_FLAG_SERIAL
+ *    appeared.  path_steps changed meaning in 4: it counts wf_shade steps only; the finisher's shade
+ *    steps, which it included before, are finish_steps (their sum is the old path_steps).
+ * 5: rt_stats_get and rt_render write the ABI-3 struct only (the 104 bytes through p1_rays, what
+ *    every binding of an ABI-3 header allocated; ABI 4 wrote past them), and the fields added in 4
+ *    reach a caller only through rt_stats_get_sized with its own sizeof(rt_stats).
+ *    RT_FLAG_SORTED_TRAVERSAL is accepted and has no effect (the octant-ordered traversal it
+ *    switched off was removed).
+ * A binding checks rt_abi_version() at load time. */
+#define RT_ABI_VERSION 5
 
 #ifdef __cplusplus
 extern "C" {
@@ -109,8 +115,8 @@ enum {
   RT_FLAG_FINISH = 16,            /* use the finisher whatever the batch size (rt_set_finish)   */
   RT_FLAG_SERIAL = 32,            /* measurement: one frame group per batch (no two groups' kernels
                                      overlap), at most one group's path state of frames per batch */
-  RT_FLAG_SORTED_TRAVERSAL = 64   /* wavefront trace: visit children by entry distance only (the exact
-                                     kernel alone, no octant-ordered fast traversal); same image */
+  RT_FLAG_SORTED_TRAVERSAL = 64   /* ABI 4 (accepted, no effect since ABI 5): the trace always visits
+                                     children by entry distance */
 };
 
 typedef struct rt_stats {
@@ -123,9 +129,10 @@ typedef struct rt_stats {
   double trace_ms;          /* summed duration of those launches (HIP events around each) */
   uint64_t trace_iters;     /* RT_FLAG_COUNT_VISITS: traversal loop iterations, all waves */
   uint64_t trace_iters_max; /* RT_FLAG_COUNT_VISITS: max loop iterations of one wave       */
-  uint64_t path_steps;      /* wavefront path: wf_shade steps (one per path per bounce pass) */
+  uint64_t path_steps;      /* wavefront path: wf_shade steps (one per path per bounce pass; since
+                               ABI 4 without the finisher's, which are finish_steps)           */
   uint64_t p1_rays;         /* wavefront path: rays traced from pass 0's 16-B ray records  */
-  /* ---- ABI 4 */
+  /* ---- ABI 4: written only by rt_stats_get_sized */
   uint64_t pass0_steps;     /* of path_steps: pass 0 (implicit camera paths)                */
   uint64_t pass1_steps;     /* of path_steps: pass 1 (paths whose rays are 16-B records)    */
   uint64_t finish_steps;    /* shade steps run by the path-persistent finisher (wf_finish)  */
@@ -203,9 +210,9 @@ int rt_set_pipeline(rt_ctx* ctx, int32_t depth);
 int rt_render_async(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames);
 /* rt_render_async + synchronise + optional stats snapshot. */
 int rt_render(rt_ctx* ctx, const rt_frame_params* params, const float* rand_origin, int32_t n_frames,
-              rt_stats* stats);
+              rt_stats* stats /* ABI-3 fields only (see rt_stats_get) */);
 int rt_synchronize(rt_ctx* ctx);
-int rt_stats_get(rt_ctx* ctx, rt_stats* stats);  /* synchronises; writes sizeof(rt_stats) of ABI 4 */
+int rt_stats_get(rt_ctx* ctx, rt_stats* stats);  /* synchronises; writes the ABI-3 fields (104 bytes) */
 /* The same, writing at most stats_bytes bytes (a caller's own, possibly older, sizeof(rt_stats)). */
 int rt_stats_get_sized(rt_ctx* ctx, rt_stats* stats, size_t stats_bytes);
 int rt_stats_reset(rt_ctx* ctx);

@@ -67,14 +67,17 @@ struct __attribute__((aligned(16))) GNode {
   int4 ref;   // left ref, right ref, -, -
 };
 // 4-wide node collapsed from the binary tree above (same exact fp32 child boxes, SoA: child k
-// in component k; an empty slot has the inverted bounds lo = +inf, hi = -inf, which the slab test
-// never hits).  128 B = one cache line; one fetch replaces about two dependent binary steps.
-// ord[o]: the fast traversal's child order for ray-direction octant o (bit a: direction component
-// a negative): nibble c = the set of children that come after child c in that order.
+// in component k; an empty slot has the inverted bounds lo = +inf, hi = -inf and the ref Q_EMPTY).
+// The sign-selected slab of a ray with a finite 1/d never hits an inverted box (t0 = +inf,
+// t1 = -inf).  The literal slab of a ray with a zero direction component takes per-axis min / max,
+// which turns the inverted box into an infinite one, so that path tests the slot's ref instead
+// (tl_qnode_keys, coop_box): entering a Q_EMPTY ref reads QNode 0x7fffffff, far outside the
+// array (the round-4 hipErrorIllegalAddress).  128 B = one cache line; one fetch
+// replaces about two dependent binary steps.
 struct __attribute__((aligned(16))) QNode {
   float4 lox, loy, loz, hix, hiy, hiz;
   int4 ref;  // child refs (QNode index or leaf ref), Q_EMPTY for an empty slot
-  uint16_t ord[8];
+  int4 pad;
 };
 static_assert(sizeof(QNode) == 128, "one cache line");
 constexpr int Q_EMPTY = 0x7fffffff;

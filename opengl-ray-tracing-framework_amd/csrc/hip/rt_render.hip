@@ -73,14 +73,29 @@ struct rt_ctx {
   unsigned int* d_counter = nullptr;
   unsigned long long* d_stats = nullptr;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;        // whole render calls
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> trace_events;  // traversal launches
+  struct TraceEv {
+    hipEvent_t s, e;
+    uint64_t call;  // the render call (its index in `launches`) that queued the launch
+  };
+  std::vector<TraceEv> trace_events;  // traversal launches
   std::vector<hipEvent_t> event_pool;
   double kernel_ms = 0.0, trace_ms = 0.0;
-  // union of the traversal launches' intervals (rt_stats.trace_busy_ms): start / end of each launch
-  // relative to t_ref (recorded on the ctx stream at creation and at every rt_stats_reset, with
-  // nothing in flight), kept as sorted disjoint intervals
-  hipEvent_t t_ref = nullptr;
-  std::vector<std::pair<double, double>> busy;
+  // Union of the traversal launches' intervals (rt_stats.trace_busy_ms).  Each folded launch is
+  // placed on a double-precision timeline by its start's offset from the previously folded
+  // launch's start (busy_anchor, at busy_anchor_t ms), so an offset is a short float interval
+  // however long the context lives.  Intervals that can no longer overlap a pending launch are
+  // summed into busy_closed_ms and dropped: a launch of call k starts after every launch of
+  // call k-2 has ended (pipelined calls wait for their set's previous call; the ctx stream joins
+  // each call's streams), so folding call k's launches closes the intervals of calls <= k-2 and
+  // the open list holds about two calls' worth.
+  struct BusyIv {
+    double lo, hi;
+    uint64_t call;  // the newest call merged into the interval
+  };
+  hipEvent_t busy_anchor = nullptr;
+  double busy_anchor_t = 0.0;
+  std::vector<BusyIv> busy;
+  double busy_closed_ms = 0.0;
   uint64_t launches = 0, trace_launches = 0;
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
@@ -95,11 +110,6 @@ struct rt_ctx {
   };
   FrameTable ft[5];
   int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
-#ifndef RT_FAST_TRACE_DEFAULT
-#define RT_FAST_TRACE_DEFAULT 0
-#endif
-  bool fast_trace = RT_FAST_TRACE_DEFAULT;    // wf_trace MODE_FAST + MODE_SLOWIN (dev: RT_FAST_TRACE=0/1)
-  bool call_fast = false;                     // this call's launches: fast_trace && !RT_FLAG_SORTED_TRAVERSAL
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
@@ -523,32 +533,6 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
         lo[k][i] = i < (int)sl.size() ? sl[i].lo[k] : pinf;
         hi[k][i] = i < (int)sl.size() ? sl[i].hi[k] : -pinf;
       }
-    // fast traversal's child order per ray-direction octant o (bit a set: component a of the
-    // direction negative): children by the projection onto the octant's diagonal, nearest first;
-    // ord[o] holds, in nibble c, the children that come after child c
-    // children by the box corner a ray of the octant enters first (dev RT_ORD_KEY=centre: by the
-    // box centre; C3 bulk -1.2%)
-    static const bool ord_corner = !(knob("RT_ORD_KEY") && strcmp(knob("RT_ORD_KEY"), "centre") == 0);
-    uint16_t ord[8];
-    for (int o = 0; o < 8; o++) {
-      double key[4];
-      for (int i = 0; i < 4; i++) {
-        key[i] = HUGE_VAL;
-        if (i < (int)sl.size()) {
-          key[i] = 0.0;
-          for (int k = 0; k < 3; k++) {
-            const bool neg = ((o >> k) & 1) != 0;
-            if (ord_corner) key[i] += neg ? -(double)sl[i].hi[k] : (double)sl[i].lo[k];
-            else key[i] += (neg ? -0.5 : 0.5) * ((double)sl[i].lo[k] + (double)sl[i].hi[k]);
-          }
-        }
-      }
-      uint32_t m = 0;
-      for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++)
-          if (j != i && (key[j] > key[i] || (key[j] == key[i] && j > i))) m |= 1u << (4 * i + j);
-      ord[o] = (uint16_t)m;
-    }
     rtd::QNode& q = qn[idx];
     q.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     q.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
@@ -557,7 +541,6 @@ bool build_wide(std::vector<GNode>& gn, int root, std::vector<float4>& trin, std
     q.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
     q.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
     q.ref = make_int4(refs[0], refs[1], refs[2], refs[3]);
-    memcpy(&q.ord, ord, sizeof(ord));
     return idx;
   };
   qroot = is_leaf(croot) ? croot : build(croot, 1);
@@ -622,11 +605,6 @@ int occupancy(rt_ctx* c) {
     const hipError_t e =
         cam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, true>, 256, c->trace_lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rtd::wf_trace<false, true, false>, 256, c->trace_lds);
-    int bf = b;  // the fast instantiation runs on the same grid
-    const hipError_t ef =
-        cam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&bf, rtd::wf_trace<false, true, true, false, false, rtd::MODE_FAST>, 256, c->trace_lds)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&bf, rtd::wf_trace<false, true, false, false, false, rtd::MODE_FAST>, 256, c->trace_lds);
-    if (ef == hipSuccess && c->fast_trace) b = std::min(b, bf);
     return e == hipSuccess ? std::max(1, b) : 1;
   };
   c->trace_bpc0 = occ(true);  // pass 0 is the implicit camera pass
@@ -663,30 +641,44 @@ int occupancy(rt_ctx* c) {
   return RT_OK;
 }
 
+// The traversal stack's overflow indices, checked on the host before every launch that uses them
+// (DESIGN.md §4, round 5): entry j in [KL, entries) of grid lane l of path-state set `set` lives at
+// element set * ovf_group + (j - KL) * ovf_lanes + l, with ovf_lanes = trace grid blocks * 256 and
+// l below that (the finisher's grid is never larger than the trace grid); a lane-quad move copies
+// at most KL + 64 entries.  entries = the deepest stack of the scene's trees (3 * qdepth + 2 for
+// the 4-wide one).
+std::string ovf_layout_error(const rt_ctx* c, int set, unsigned int trace_grid_blocks) {
+  const int entries = std::max(c->stack_entries, c->qstack_entries);
+  const int kl = c->trace_lds_entries;
+  const size_t rows = (size_t)std::max(0, entries - kl);
+  const size_t lanes = (size_t)trace_grid_blocks * 256u;
+  const size_t per_set = c->stack_ovf_bytes / sizeof(int2) / (size_t)std::max(1, c->n_groups);
+  char buf[256];
+  if (set < 0 || set >= c->n_groups) {
+    snprintf(buf, sizeof buf, "overflow stack: path-state set %d of %d", set, c->n_groups);
+    return buf;
+  }
+  if (rows > 0 && (!c->d_stack_ovf || rows * lanes > per_set)) {
+    snprintf(buf, sizeof buf, "overflow stack: %zu rows x %zu lanes exceed %zu entries per set", rows, lanes, per_set);
+    return buf;
+  }
+  if ((unsigned)(c->finish_bpc * c->n_cus) > trace_grid_blocks || c->pipe_finish_bpc > c->finish_bpc) {
+    snprintf(buf, sizeof buf, "overflow stack: finisher grid %d x %d above the trace grid %u", c->finish_bpc,
+             c->n_cus, trace_grid_blocks);
+    return buf;
+  }
+  if (entries > kl + 64) {
+    snprintf(buf, sizeof buf, "overflow stack: %d entries, a lane-quad move copies %d", entries, kl + 64);
+    return buf;
+  }
+  return std::string();
+}
+
 template <bool COUNT, bool WIDE>
 void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t st, bool small) {
   // pass 1 reads the 16-B rays pass 0 queued (WFState::org) in an instantiation of its own, so the
   // later passes' kernel carries none of it
   const bool p1 = !WP.cam_n && WP.pass == 1 && WP.p1_compact;
-  if (WIDE && c->call_fast) {
-    // fast traversal, then the exact kernel over the rays it deferred (zero direction components,
-    // exact distance ties: usually none, and its blocks exit at once).  COUNT: the visit counts
-    // (and the tile-cost probes) are those of the traversal that runs
-    constexpr int F = rtd::MODE_FAST, SL = rtd::MODE_SLOWIN;
-    if (small && !COUNT) {  // static first shares of mid-size passes
-      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, false, F>), grid, dim3(256), c->trace_lds, st, WP);
-    } else {
-      if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, true, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, true, F>), grid, dim3(256), c->trace_lds, st, WP);
-      else hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, false, F>), grid, dim3(256), c->trace_lds, st, WP);
-    }
-    if (WP.cam_n) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, true, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
-    else if (p1) hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, true, SL>), grid, dim3(256), c->trace_lds, st, WP);
-    else hipLaunchKernelGGL((rtd::wf_trace<COUNT, true, false, false, false, SL>), grid, dim3(256), c->trace_lds, st, WP);
-    return;
-  }
   if (small && !COUNT && WIDE) {  // static first shares of mid-size passes
     if (WP.cam_n)
       hipLaunchKernelGGL((rtd::wf_trace<false, true, true, true>), grid, dim3(256), c->trace_lds, st, WP);
@@ -730,45 +722,75 @@ hipEvent_t take_event(rt_ctx* c) {
 // Timing events of launches not yet folded into kernel_ms / trace_ms: a front end that never
 // calls rt_synchronize (it waits on its own stream or events) would otherwise grow these lists
 // without bound.  Past `cap` pending pairs, the oldest are waited for, folded and recycled.
-// a finished launch's (start, end) events: its duration into acc_ms and, for traversal launches
-// (busy), its interval into the union c->busy
-int fold_pair(rt_ctx* c, const std::pair<hipEvent_t, hipEvent_t>& e, double& acc_ms, bool busy) {
+// a finished render call's (start, end) events: its duration into acc_ms
+int fold_pair(rt_ctx* c, const std::pair<hipEvent_t, hipEvent_t>& e, double& acc_ms) {
   float ms = 0.0f;
   HIPCHK(c, hipEventElapsedTime(&ms, e.first, e.second));
   acc_ms += ms;
-  if (busy && c->t_ref) {
-    float a = 0.0f, b = 0.0f;
-    HIPCHK(c, hipEventElapsedTime(&a, c->t_ref, e.first));
-    HIPCHK(c, hipEventElapsedTime(&b, c->t_ref, e.second));
-    double lo = a, hi = std::max(a, b);
-    auto& v = c->busy;
-    // merge [lo, hi] into the sorted disjoint list (launches arrive nearly in time order)
-    auto it = std::upper_bound(v.begin(), v.end(), std::make_pair(lo, hi));
-    if (it != v.begin() && std::prev(it)->second >= lo) {
-      --it;
-      lo = it->first;
-      hi = std::max(hi, it->second);
-      it = v.erase(it);
-    }
-    while (it != v.end() && it->first <= hi) {
-      hi = std::max(hi, it->second);
-      it = v.erase(it);
-    }
-    v.insert(it, std::make_pair(lo, hi));
-  }
   c->event_pool.push_back(e.first);
   c->event_pool.push_back(e.second);
   return RT_OK;
 }
+// a finished traversal launch: its duration into trace_ms and its interval into the union
+// (rt_ctx::busy; pairs arrive in queue order)
+int fold_trace(rt_ctx* c, const rt_ctx::TraceEv& e) {
+  float ms = 0.0f, a = 0.0f;
+  HIPCHK(c, hipEventElapsedTime(&ms, e.s, e.e));
+  c->trace_ms += ms;
+  if (c->busy_anchor) HIPCHK(c, hipEventElapsedTime(&a, c->busy_anchor, e.s));
+  double lo = c->busy_anchor_t + (double)a, hi = lo + (double)std::max(ms, 0.0f);
+  if (c->busy_anchor) c->event_pool.push_back(c->busy_anchor);
+  c->busy_anchor = e.s;  // this launch's start is the next one's reference
+  c->busy_anchor_t = lo;
+  c->event_pool.push_back(e.e);
+  auto& v = c->busy;
+  // close what no pending launch can overlap any more (calls <= e.call - 2)
+  size_t keep = 0;
+  for (const auto& iv : v) {
+    if (iv.call + 2 <= e.call) c->busy_closed_ms += iv.hi - iv.lo;
+    else v[keep++] = iv;
+  }
+  v.resize(keep);
+  // merge [lo, hi] into the sorted disjoint list
+  uint64_t call = e.call;
+  auto it = std::upper_bound(v.begin(), v.end(), lo, [](double x, const rt_ctx::BusyIv& iv) { return x < iv.lo; });
+  if (it != v.begin() && std::prev(it)->hi >= lo) {
+    --it;
+    lo = it->lo;
+    hi = std::max(hi, it->hi);
+    call = std::max(call, it->call);
+    it = v.erase(it);
+  }
+  while (it != v.end() && it->lo <= hi) {
+    hi = std::max(hi, it->hi);
+    call = std::max(call, it->call);
+    it = v.erase(it);
+  }
+  v.insert(it, rt_ctx::BusyIv{lo, hi, call});
+  return RT_OK;
+}
 
-int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap, bool busy) {
+// Past `cap` pending pairs, the oldest are waited for, folded and recycled.  Pairs of one call can
+// sit on different streams (frame / pixel groups, pipelined sets), so each pair is waited for
+// itself (in queue order: cheap once the first is done).
+int fold_events(rt_ctx* c, std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double& acc_ms, size_t cap) {
   if (ev.size() <= cap) return RT_OK;
   const size_t n = ev.size() - cap / 2;
   for (size_t i = 0; i < n; i++) {
-    // pairs of one call can sit on different streams (frame / pixel groups, pipelined sets), so
-    // each pair is waited for itself (in queue order: cheap once the first is done)
     HIPCHK(c, hipEventSynchronize(ev[i].second));
-    const int rc = fold_pair(c, ev[i], acc_ms, busy);
+    const int rc = fold_pair(c, ev[i], acc_ms);
+    if (rc) return rc;
+  }
+  ev.erase(ev.begin(), ev.begin() + (ptrdiff_t)n);
+  return RT_OK;
+}
+int fold_trace_events(rt_ctx* c, size_t cap) {
+  auto& ev = c->trace_events;
+  if (ev.size() <= cap) return RT_OK;
+  const size_t n = ev.size() - cap / 2;
+  for (size_t i = 0; i < n; i++) {
+    HIPCHK(c, hipEventSynchronize(ev[i].e));
+    const int rc = fold_trace(c, ev[i]);
     if (rc) return rc;
   }
   ev.erase(ev.begin(), ev.begin() + (ptrdiff_t)n);
@@ -849,10 +871,8 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = knob("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
-  if (const char* e = knob("RT_FAST_TRACE")) c->fast_trace = atoi(e) != 0;
   if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess || hipEventCreate(&c->t_ref) != hipSuccess ||
-      hipEventRecord(c->t_ref, c->stream) != hipSuccess) {
+      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -868,7 +888,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
-  if (c->t_ref) (void)hipEventDestroy(c->t_ref);
+  if (c->busy_anchor) (void)hipEventDestroy(c->busy_anchor);
   dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trx); dfree(c->d_trin); dfree(c->d_mats);
   for (auto& t : c->light) {
     dfree(t.d);
@@ -876,7 +896,7 @@ int rt_destroy(rt_ctx* c) {
     if (t.built) (void)hipEventDestroy(t.built);
   }
   dfree(c->d_hdr); dfree(c->d_cache); dfree(c->d_accum); dfree(c->d_counter); dfree(c->d_stats);
-  for (auto& e : c->trace_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->trace_events) { (void)hipEventDestroy(e.s); (void)hipEventDestroy(e.e); }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->wf_mem) (void)hipFree(c->wf_mem);
   for (auto& a : c->aux) if (a) (void)hipStreamDestroy(a);
@@ -1304,7 +1324,6 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
   const int pipe_sets = std::min(c->pipe_depth, c->n_groups);
   const size_t nv = std::max<size_t>(1, (size_t)c->n_valid);
   const bool serial = (fp->flags & RT_FLAG_SERIAL) != 0 && !(fp->flags & RT_FLAG_MEGAKERNEL);
-  c->call_fast = c->fast_trace && !(fp->flags & RT_FLAG_SORTED_TRAVERSAL);
   bool pipe = pipe_sets >= 2 && !(fp->flags & RT_FLAG_MEGAKERNEL) && !serial && n_trace_pre > 0 &&
               c->n_valid >= 64 * c->n_groups && !c->tile_cost_on &&
               (n_trace_pre < c->n_groups ||
@@ -1565,6 +1584,10 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
                       (pipe ? (size_t)pset * (size_t)c->n_valid : 0);
         WP.K.stack_ovf = c->d_stack_ovf ? c->d_stack_ovf + (size_t)set * ovf_group : nullptr;
         WP.K.ovf_lanes = trace_grid * 256u;
+        {
+          const std::string e = ovf_layout_error(c, set, trace_grid);
+          if (!e.empty()) return fail(c, RT_ERR_STATE, e);
+        }
         WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds (RT_DEBUG_PASSES)
         WP.S = c->wfg[set];
         WP.S.pix_xy = c->wf.pix_xy + w0;
@@ -1697,7 +1720,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           launch_trace(c, count, dim3(pass == 0 ? trace_grid0 : trace_grid1), WP, sg[g], slots_g[g] <= c->finish_slots);
           HIPCHK(c, hipGetLastError());
           HIPCHK(c, hipEventRecord(t1, sg[g]));
-          c->trace_events.push_back({t0, t1});
+          c->trace_events.push_back({t0, t1, c->launches});
           c->trace_launches++;
 #ifdef RT_DEV
           if (debug_passes) {  // development aid: per-pass rays / visits / duration (syncs!)
@@ -1813,8 +1836,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     HIPCHK(c, hipEventRecord(LT->last_use, c->stream));
     c->events.push_back({e0, e1});
     c->launches++;
-    int frc = fold_events(c, c->trace_events, c->trace_ms, kMaxPendingEvents, true);
-    if (!frc) frc = fold_events(c, c->events, c->kernel_ms, kMaxPendingEvents, false);
+    int frc = fold_trace_events(c, kMaxPendingEvents);
+    if (!frc) frc = fold_events(c, c->events, c->kernel_ms, kMaxPendingEvents);
     if (frc) return frc;
   }
   return RT_OK;
@@ -1826,12 +1849,12 @@ int rt_synchronize(rt_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // (the stream joins every group and pipelined set of each call, so all pairs have finished)
   for (auto& e : c->events) {
-    const int rc = fold_pair(c, e, c->kernel_ms, false);
+    const int rc = fold_pair(c, e, c->kernel_ms);
     if (rc) return rc;
   }
   c->events.clear();
   for (auto& e : c->trace_events) {
-    const int rc = fold_pair(c, e, c->trace_ms, true);
+    const int rc = fold_trace(c, e);
     if (rc) return rc;
   }
   c->trace_events.clear();
@@ -1840,16 +1863,25 @@ int rt_synchronize(rt_ctx* c) {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+// rt_stats_get and rt_render write the ABI-3 struct (through p1_rays), the size every binding of
+// that header allocated; the fields added since reach a caller only through rt_stats_get_sized
+// with its own sizeof(rt_stats)
+constexpr size_t kStatsBytesAbi3 = offsetof(rt_stats, pass0_steps);
+static_assert(kStatsBytesAbi3 == 13 * 8, "the ABI-3 rt_stats is 13 eight-byte fields");
+int stats_fill(rt_ctx* c, rt_stats* st);
+
 int rt_stats_get_sized(rt_ctx* c, rt_stats* st, size_t bytes) {
   if (!c || !st) return RT_ERR_ARG;
   rt_stats full;
-  const int rc = rt_stats_get(c, &full);
+  const int rc = stats_fill(c, &full);
   if (rc) return rc;
   memcpy(st, &full, std::min(bytes, sizeof(full)));
   return RT_OK;
 }
 
-int rt_stats_get(rt_ctx* c, rt_stats* st) {
+int rt_stats_get(rt_ctx* c, rt_stats* st) { return rt_stats_get_sized(c, st, kStatsBytesAbi3); }
+
+int stats_fill(rt_ctx* c, rt_stats* st) {
   if (!c || !st) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
@@ -1870,8 +1902,8 @@ int rt_stats_get(rt_ctx* c, rt_stats* st) {
   st->pass0_steps = ps[2];
   st->pass1_steps = ps[3];
   st->finish_steps = ps[4];
-  double busy = 0.0;
-  for (const auto& iv : c->busy) busy += iv.second - iv.first;
+  double busy = c->busy_closed_ms;
+  for (const auto& iv : c->busy) busy += iv.hi - iv.lo;
   st->trace_busy_ms = busy;
   return RT_OK;
 }
@@ -1886,7 +1918,7 @@ int rt_stats_reset(rt_ctx* c) {
   c->trace_ms = 0.0;
   c->trace_launches = 0;
   c->busy.clear();
-  if (c->t_ref) HIPCHK(c, hipEventRecord(c->t_ref, c->stream));  // nothing in flight (synchronised)
+  c->busy_closed_ms = 0.0;
   return RT_OK;
 }
 

@@ -29,16 +29,6 @@ namespace rtd {
 
 // RT_CHECK (development build: make variant HIPEXTRA=-DRT_CHECK): bounds checks that report the
 // first bad index of a launch with printf and replace it with a harmless one instead of faulting
-#ifdef RT_CHECK
-#define RT_CHK(cond, fmt, ...)                                                     \
-  do {                                                                             \
-    if (!(cond)) {                                                                 \
-      printf("[rt check] %s:%d " fmt "\n", __FILE__, __LINE__, ##__VA_ARGS__);   \
-    }                                                                              \
-  } while (0)
-#else
-#define RT_CHK(cond, fmt, ...) do { } while (0)
-#endif
 
 // per-path flags (< 256: packed with the bounce in s5.y)
 enum : uint32_t {
@@ -316,9 +306,6 @@ struct TraceLane {
   RTD float limit(float eps) const { return cull_limit(best, eps, ix, iy, iz); }
   int besttri, sp, cur, tri_i, tri_end;
   int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
-  // fast traversal: the near-plane offsets packed in bytes 0-2 (far = near ^ 48 / 80 / 112) and
-  // 2 x the octant of d in byte 3 (QNode::ord[octant] at 112 + that)
-  uint32_t offPk;
   bool haveCur, anyhit, finite;
 };
 
@@ -637,121 +624,6 @@ RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
   }
   return tl_qnode_push<POP>(P, L, S, cull, k, r);
 }
-// ---- fast traversal (wf_trace MODE_FAST): rays with a finite 1/d and no exact distance tie; the
-// rest are deferred to the exact kernel (MODE_SLOWIN), which traces them from scratch.
-// The kept children of a node are pushed in the node's precomputed order for the ray's direction
-// octant (QNode::ord) instead of being sorted by entry distance: every child's stack position is
-// the number of kept children that come after it (a popcount of its ord nibble against the kept
-// mask), so the four stores are unconditional (an unkept child lands on a free slot above the new
-// top) and the nearest kept child is simply the top, which the iteration's single pop takes.
-// Order only decides how soon `best` tightens: the closest hit stays exact (culling bound, ties
-// deferred), DESIGN.md §2.
-RTD void tl_store(const TraceStack& S, int idx, int2 ent) {  // the entry at stack index idx
-  if (idx < S.KL) S.lds[idx * TL_LANES] = ent;
-  else *S.ovf_at(idx) = pack_ent(ent);
-}
-#ifndef RT_FAST_POP_NEAR  // 1: the nearest kept child is pushed too and taken by the single pop
-#define RT_FAST_POP_NEAR 0
-#endif
-// returns true when no child was entered (the caller pops)
-RTD bool tl_qnode_fast(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
-#ifdef RT_CHECK
-  if ((unsigned)L.cur >= (unsigned)P.n_qnodes) {
-    printf("[rt check] fast node %d of %d (sp %d)\n", L.cur, P.n_qnodes, L.sp);
-    L.cur = 0;
-  }
-#endif
-  const uint32_t off = (uint32_t)L.cur << 7;  // (low 7 bits zero: | adds an in-node offset)
-  const uint32_t pk = L.offPk;
-  const int4 rf = ld<int4>(P.qnodes, off + 96u);
-  const uint32_t M = ld<unsigned short>(P.qnodes, (off | (pk >> 24)) + 112u);
-  const uint32_t ax = off | (pk & 0xffu), ay = off | ((pk >> 8) & 0xffu), az = off | ((pk >> 16) & 0xffu);
-  const float4 nx = ld<float4>(P.qnodes, ax), ny = ld<float4>(P.qnodes, ay), nz = ld<float4>(P.qnodes, az);
-  const float4 fx = ld<float4>(P.qnodes, ax ^ 48u), fy = ld<float4>(P.qnodes, ay ^ 80u), fz = ld<float4>(P.qnodes, az ^ 112u);
-  float t0[4], t1[4];
-  tl_qnode_t01(L, nx, ny, nz, fx, fy, fz, t0, t1);
-  const float lim = cull ? L.limit(P.cull_eps) : __int_as_float(0x7f800000);
-  // hit (t1 >= t0 && t1 > 0, RT:315) and not culled (t0 <= lim): with the smallest positive float
-  // dmin and lim > 0, exactly max(t0, dmin) <= min(t1, lim) (an empty slot: t0 = +inf, t1 = -inf)
-  const float dmin = __int_as_float(1);
-  bool ok[4];
-  uint32_t kept = 0u;
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    ok[c] = max_(t0[c], dmin) <= min_(t1[c], lim);
-    kept |= ok[c] ? (1u << c) : 0u;
-  }
-  const int n = __popc(kept);
-  const uint32_t A = M & (kept * 0x1111u);
-  const int r[4] = {rf.x, rf.y, rf.z, rf.w};
-  int f[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) f[c] = ok[c] ? __popc((A >> (4 * c)) & 15u) : n;
-  if (L.sp + 4 <= S.KL) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) S.lds[(L.sp + f[c]) * TL_LANES] = make_int2(r[c], __float_as_int(t0[c]));
-  } else {
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      if (ok[c]) tl_store(S, L.sp + f[c], make_int2(r[c], __float_as_int(t0[c])));
-  }
-  if (RT_FAST_POP_NEAR) {
-    L.sp += n;
-    return true;
-  }
-  // the nearest kept child (position n - 1, stored above the new top) is entered at once
-  const int top = n - 1;
-  L.cur = f[0] == top ? r[0] : f[1] == top ? r[1] : f[2] == top ? r[2] : r[3];
-  L.sp += max(top, 0);
-  return n == 0;
-}
-#ifndef RT_FAST_DEFER_EDGES  // fast traversal: a point the edge filter cannot decide defers the ray (1) or
-                             // runs the reference's edge functions in place (0)
-#define RT_FAST_DEFER_EDGES 0
-#endif
-// one triangle for the fast traversal: 0 no closer hit, 1 the new closest hit, 2 defer the ray (an
-// exact distance tie with the current best, whose order rule tie_wins lives in the exact kernel)
-RTD int tl_triangle_fast(const KParams& P, TraceLane& L, int i) {
-#ifdef RT_CHECK
-  if ((unsigned)i >= (unsigned)P.n_tri) {
-    printf("[rt check] fast triangle %d of %d\n", i, P.n_tri);
-    i = 0;
-  }
-#endif
-  const uint32_t off = (uint32_t)i * 48u;
-  const float4 A = ld<float4>(P.trx, off), B = ld<float4>(P.trx, off + 16u), Cc = ld<float4>(P.trx, off + 32u);
-  const f3 p1 = xyz(A);
-  const f3 ng = mk3(A.w, B.w, Cc.w);
-  const float dn = dot(ng, L.d());
-  const float num = dot(ng, p1) - dot(L.o(), ng);
-  const float t = num / dot(L.d(), ng);                                // RT:265
-  const float dist = t - 0.00001f;
-  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (dist <= L.best);  // RT:262, 268, 328/356
-  const f3 Pp = L.o() + L.d() * t;
-  const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
-  const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
-  const float b3 = __builtin_fmaf(Cc.x, qx, __builtin_fmaf(Cc.y, qy, Cc.z * qz));
-  const float b1 = (1.0f - b2) - b3;
-  const float mn = fminf(b1, fminf(b2, b3));
-  const float dq = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
-  const float lr = fmaxf(fabsf(B.x), fmaxf(fabsf(B.y), fabsf(B.z))) + fmaxf(fabsf(Cc.x), fmaxf(fabsf(Cc.y), fabsf(Cc.z)));
-  const float m = (dq * lr) * P.tri_k1 + P.tri_k0;
-  bool inside = mn > 0.0f;
-  const bool undecided = ok & !((fabsf(mn) > m) & (m < 0.25f));
-  if (RT_FAST_DEFER_EDGES) {
-    if (undecided) return 2;
-  } else if (undecided) {
-    inside = tl_edges_exact(P, i, p1, ng, Pp);
-  }
-  ok &= inside;
-  if (!ok) return 0;
-  if (dist == L.best) return 2;
-  L.best = dist;
-  L.besttri = i;
-  L.bestt = t;
-  return 1;
-}
-
 // the node fetch alone (the finisher issues it before its triangle test): rf + six planes, near /
 // far for a finite 1/d, lo / hi otherwise (tl_start's offsets cover both)
 struct QLoad {
@@ -788,8 +660,6 @@ RTD void tl_start(const KParams& P, TraceLane& L) {
   L.offNx = (L.ix > 0.0f || !L.finite) ? 0 : 48;
   L.offNy = (L.iy > 0.0f || !L.finite) ? 16 : 64;
   L.offNz = (L.iz > 0.0f || !L.finite) ? 32 : 80;
-  L.offPk = (uint32_t)L.offNx | (uint32_t)L.offNy << 8 | (uint32_t)L.offNz << 16 |
-            (uint32_t)(2 * ((L.ix < 0.0f ? 1 : 0) | (L.iy < 0.0f ? 2 : 0) | (L.iz < 0.0f ? 4 : 0))) << 24;
   L.best = INF;
   L.besttri = -1;
   L.bestt = 0.0f;
@@ -1056,7 +926,6 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
   L.sp = sp_src; L.cur = __shfl(L.cur, src);
   L.tri_i = __shfl(L.tri_i, src); L.tri_end = __shfl(L.tri_end, src);
   L.offNx = __shfl(L.offNx, src); L.offNy = __shfl(L.offNy, src); L.offNz = __shfl(L.offNz, src);
-  L.offPk = (uint32_t)__shfl((int)L.offPk, src);
   L.haveCur = __shfl((int)L.haveCur, src) != 0;
   L.anyhit = __shfl((int)L.anyhit, src) != 0;
   L.finite = __shfl((int)L.finite, src) != 0;
@@ -1087,9 +956,6 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                        // from 32 paths in the finisher cost 2-3% (profiles/r04_ab_single_coop_trace_tails_pairs_C3.log)
 #define RT_TRACE_COOP 16
 #endif
-#ifndef RT_TRACE_COOP_BULK  // the same in the large passes' kernels (1: on)
-#define RT_TRACE_COOP_BULK 0
-#endif
 #ifndef RT_RES_NT  // wf_trace writes its results with non-temporal stores (1): C3 bulk +0.45%
                    // (profiles/r04_ab_bulk_result_nt_C3.log); its HBM writes stay ~30 B per ray
                    // (scattered 4-B results and 8-B overflow-stack entries, each a partial sector)
@@ -1101,30 +967,20 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
 // passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
 // a separate instantiation: the code alone cost the bulk's kernels 0.4%).
-// MODE: MODE_EXACT traces every ray of the pass with the exact order rules (distance-sorted pushes,
-// tie_wins, the literal slab for a zero direction component); MODE_FAST (the 4-wide tree, no visit
-// counting) traces the rays with a finite 1/d in octant order (tl_qnode_fast) and defers a ray
-// with a zero direction component or an exact distance tie to the slow list (the pass's free
-// queue buffer, queue[qin ^ 1], count cnt[5]); MODE_SLOWIN is the exact kernel over that list
-// (claim counter cnt[6]), launched right after the fast one.
-enum { MODE_EXACT = 0, MODE_FAST = 1, MODE_SLOWIN = 2 };
-template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false, int MODE = MODE_EXACT>  // P1: pass 1's 16-B rays
+template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false>  // P1: pass 1's 16-B rays
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
-  static_assert(MODE == MODE_EXACT || WIDE, "fast / slow-list modes: 4-wide tree");
-  static_assert(MODE != MODE_SLOWIN || !STATIC, "the slow list is claimed dynamically");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int qin = W.pass & 1;
-  int* const slow_list = S.queue[qin ^ 1];  // free during this pass's traversal (the next shade fills it)
-  const unsigned int nq = MODE == MODE_SLOWIN ? S.cnt[5] : CAM ? W.cam_n : S.cnt[qin];
+  const unsigned int nq = CAM ? W.cam_n : S.cnt[qin];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
     S.cnt[qin ^ 1] = 0u;
     S.cnt[2 + (qin ^ 1)] = 0u;
   }
   if (nq == 0u || !P.has_scene) {
-    if (!P.has_scene && MODE != MODE_SLOWIN) {  // empty scene: every ray misses (RT:346 reads a zero node)
+    if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
       for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
         const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
         S.res[e] = -1;
@@ -1194,7 +1050,7 @@ void wf_trace(const WFParams W) {
       if (pool_next >= pool_end) {
         const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&S.cnt[MODE == MODE_SLOWIN ? 6 : 4], chunk);
+        if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
         base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= nq) {
           drained = true;
@@ -1210,7 +1066,7 @@ void wf_trace(const WFParams W) {
         if (!busy && rank < avail) {
           const unsigned int qi = pool_next + rank;
           if (CAM) {  // implicit camera pass: queue entry i is slot i's camera ray
-            const unsigned int slot = MODE == MODE_SLOWIN ? (unsigned int)slow_list[qi] >> 1 : qi;
+            const unsigned int slot = qi;
             entry = (int)(slot << 1);
             L.anyhit = false;
             uint32_t seed_unused, frame_unused;
@@ -1218,7 +1074,7 @@ void wf_trace(const WFParams W) {
             L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
             L.dx = d.x; L.dy = d.y; L.dz = d.z;
           } else {
-            entry = MODE == MODE_SLOWIN ? slow_list[qi] : S.queue[qin][qi];
+            entry = S.queue[qin][qi];
             const int path = entry >> 1;
             L.anyhit = (entry & 1) != 0;
             const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
@@ -1233,17 +1089,13 @@ void wf_trace(const WFParams W) {
           }
           tl_start<WIDE>(P, L);
           busy = true;
-          if (MODE == MODE_FAST && !L.finite) {  // a zero direction component: the literal slab (exact kernel)
-            slow_list[atomicAdd(&S.cnt[5], 1u)] = entry;
-            busy = false;
-          }
         }
         pool_next += min((unsigned int)__popcll(idle), avail);
       }
     }
     // a drained wave (queue and pool empty) with at most RT_TRACE_COOP rays left traces them with
     // four lanes each (tl_coop_step, as in wf_finish): the pass ends on its longest rays
-    if (RT_TRACE_COOP && (STATIC || (RT_TRACE_COOP_BULK && !COUNT)) && WIDE && MODE == MODE_EXACT && !coop && drained &&
+    if (RT_TRACE_COOP && STATIC && WIDE && !coop && drained &&
         pool_next >= pool_end) {
       const unsigned long long live = __ballot(busy);
       const int nl = __popcll(live);
@@ -1255,49 +1107,11 @@ void wf_trace(const WFParams W) {
         busy = (lane >> 2) < nl && b_src != 0;
       }
     }
-    // (MODE_FAST: every ray the refill handed out may have been deferred, and the pool goes on:
-    // the iteration then does nothing and the next one refills)
-    if (!__any(busy) && (MODE != MODE_FAST || drained)) break;
+    if (!__any(busy)) break;
     if (COUNT) { v_itO++; if (busy) v_busyO++; }
     bool finished = false;
-    bool defer = false;  // MODE_FAST: the ray goes to the slow list
     if (COUNT) { v_itN++; v_itT++; }
-    if (MODE == MODE_FAST && busy) {
-      // one triangle of the current leaf and one node step, then the iteration's single pop: a
-      // taken leaf, or the node's nearest kept child (the top of the stack after the pushes)
-      if (L.tri_i < L.tri_end) {
-        if (COUNT) { v_tri++; ray_steps++; }
-        const int h = tl_triangle_fast(P, L, L.tri_i++);
-        if (h == 2) {
-          finished = defer = true;
-        } else if (h == 1 && L.anyhit) {
-          finished = true;
-          L.tri_end = L.tri_i;
-        }
-      }
-      bool needPop = false;
-      if (!finished && L.haveCur) {
-        if (ref_is_leaf(L.cur)) {
-          if (L.tri_i >= L.tri_end) {  // triangle cursor free: take the leaf, move on
-            if (COUNT) { v_leaf++; v_park++; }
-            L.tri_i = leaf_first(L.cur);
-            L.tri_end = L.tri_i + leaf_count(L.cur);
-#ifdef RT_CHECK
-            if (L.tri_end > P.n_tri) {
-              printf("[rt check] leaf ref %x: triangles %d..%d of %d\n", L.cur, L.tri_i, L.tri_end, P.n_tri);
-              L.tri_i = L.tri_end = 0;
-            }
-#endif
-            needPop = true;
-          }
-        } else {
-          if (COUNT) { v_int++; ray_steps++; }
-          needPop = tl_qnode_fast(P, L, TS, cull);
-        }
-      }
-      if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
-      if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
-    } else if (RT_TRACE_COOP && (STATIC || (RT_TRACE_COOP_BULK && !COUNT)) && WIDE && MODE == MODE_EXACT && coop) {
+    if (RT_TRACE_COOP && STATIC && WIDE && coop) {
       if (busy) finished = tl_coop_step<4>(P, L, TS, cull, lane & 3);
     } else if (busy) {
       if (L.tri_i < L.tri_end) {
@@ -1332,10 +1146,6 @@ void wf_trace(const WFParams W) {
       }
       if (needPop) L.haveCur = tl_pop(P, L, TS, cull);
       if (!finished && !L.haveCur && L.tri_i >= L.tri_end) finished = true;
-    }
-    if (MODE == MODE_FAST && busy && defer) {
-      slow_list[atomicAdd(&S.cnt[5], 1u)] = entry;
-      busy = false;
     }
     if (busy && finished) {
       if (RT_RES_NT) __builtin_nontemporal_store(L.besttri, &S.res[entry]);
@@ -1780,8 +1590,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.cnt[4] = 0u;  // fetch counter of the next trace pass
-    S.cnt[5] = 0u;  // its slow list (MODE_FAST -> MODE_SLOWIN) and that list's claim counter
-    S.cnt[6] = 0u;
     if (na) {
       atomicAdd(&P.stats[16], (unsigned long long)na);  // path shade steps (rt_stats.path_steps)
       if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
@@ -1891,12 +1699,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 #ifndef RT_FINISH_SHADE_MIN  // lanes waiting for a shade step before the wave runs one
 #define RT_FINISH_SHADE_MIN 16
 #endif
-#ifndef RT_FINISH_RELOAD
-#define RT_FINISH_RELOAD 1
-#endif
-#ifndef RT_FINISH_HOLD_CONT  // the continuation ray fetched with the shadow ray, held in registers
-#define RT_FINISH_HOLD_CONT 1
-#endif
 #ifndef RT_FINISH_PRIO  // wave priority 3 / 2 / 1 / 0 above this many / half / a quarter / fewer lanes holding a
 // path: the finisher is issue-bound while its waves share the SIMDs, and half of its wave time is
 // waves with <= 16 paths left, so full waves (the long bounce chains of costly pixels) go first.
@@ -1908,9 +1710,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // -5.7 / -4.1% (the shade batch at 16 lanes), 16 with the shade batch at 64 lanes -6.6%
 // (profiles/r04_ab_single_coop_finisher_w3_C3.log)
 #define RT_FINISH_COOP 16
-#endif
-#ifndef RT_FINISH_COOP2  // ... and with at most this many (<= 32), two lanes per path until 16 are left (0: off)
-#define RT_FINISH_COOP2 0
 #endif
 #ifndef RT_FINISH_COOP_SHADE_MIN  // the same in coop mode, in lanes (four per path): a wave of <= 16 paths
 // shades once all of them wait (or none traces)
@@ -1932,9 +1731,6 @@ void wf_finish(const WFParams W) {
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
-#if !RT_FINISH_RELOAD
-  const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
-#endif
   TraceStack TS;
   TS.KL = P.lds_entries;
   TS.lds0 = reinterpret_cast<int2*>(smem);
@@ -1952,7 +1748,7 @@ void wf_finish(const WFParams W) {
   enum : int { FS_IDLE = 0, FS_TRACE = 1, FS_SHADE = 2 };
   int st = FS_IDLE, path = 0;
   bool drained = false, contNext = false;
-  int coop = 0;  // lanes per path: 0 (one), 2 (RT_FINISH_COOP2) or 4 (RT_FINISH_COOP); wave-uniform
+  int coop = 0;  // lanes per path: 0 (one) or 4 (RT_FINISH_COOP); wave-uniform
   auto lead = [&]() { return coop == 0 || (lane & (coop - 1)) == 0; };  // counts for its group
   TraceLane L;
   L.anyhit = false;
@@ -1967,7 +1763,7 @@ void wf_finish(const WFParams W) {
     L.anyhit = sh;
     const float4 oa = sh ? S.sa[path] : S.ra[path];
     const float2 ob = sh ? S.sb[path] : S.rb[path];
-    if (RT_FINISH_HOLD_CONT && contNext) {
+    if (contNext) {
       ca = S.ra[path];
       cb = S.rb[path];
     }
@@ -1976,10 +1772,6 @@ void wf_finish(const WFParams W) {
     tl_start<WIDE>(P, L);
   };
   auto begin_cont = [&]() {
-    if (!RT_FINISH_HOLD_CONT) {
-      begin_rays(false, true);
-      return;
-    }
     contNext = false;
     L.anyhit = false;
     L.ox = ca.x; L.oy = ca.y; L.oz = ca.z;
@@ -2007,16 +1799,15 @@ void wf_finish(const WFParams W) {
       drained = base + want >= na;
     }
 #if RT_FINISH_COOP
-    if (WIDE && coop < 4 && drained) {
-      // paths left: one per lane, or one per group of the current coop mode
-      const unsigned long long live = __ballot(st != FS_IDLE && lead());
+    if (WIDE && coop == 0 && drained) {
+      // paths left: one per lane
+      const unsigned long long live = __ballot(st != FS_IDLE);
       const int nl = __popcll(live);
-      const int G = nl <= RT_FINISH_COOP ? 4 : (coop == 0 && nl <= RT_FINISH_COOP2) ? 2 : 0;
-      if (nl > 0 && G > coop) {
-        // the g-th path moves to lanes G*g .. G*g+G-1
-        const int src = G == 4 ? coop_move<4>(L, TS, live, lane) : coop_move<2>(L, TS, live, lane);
-        const int g = lane / G;
-        coop = G;
+      if (nl > 0 && nl <= RT_FINISH_COOP) {
+        // the g-th path moves to lanes 4g .. 4g+3
+        const int src = coop_move<4>(L, TS, live, lane);
+        const int g = lane / 4;
+        coop = 4;
         path = __shfl(path, src);
         contNext = __shfl((int)contNext, src) != 0;
         ca.x = __shfl(ca.x, src); ca.y = __shfl(ca.y, src); ca.z = __shfl(ca.z, src); ca.w = __shfl(ca.w, src);
@@ -2049,9 +1840,8 @@ void wf_finish(const WFParams W) {
       }
 #endif
       if (st == FS_TRACE &&
-          (!P.has_scene || (RT_FINISH_COOP && WIDE && coop == 4   ? tl_coop_step<4>(P, L, TS, cull, lane & 3)
-                            : RT_FINISH_COOP && WIDE && coop == 2 ? tl_coop_step<2>(P, L, TS, cull, lane & 1)
-                                                                  : tl_step_prefetch<WIDE>(P, L, TS, cull)))) {
+          (!P.has_scene || (RT_FINISH_COOP && WIDE && coop == 4 ? tl_coop_step<4>(P, L, TS, cull, lane & 3)
+                                                                : tl_step_prefetch<WIDE>(P, L, TS, cull)))) {
         S.res[2 * path + (L.anyhit ? 1 : 0)] = L.besttri;
         if (lead()) nrays++;
         if (contNext) begin_cont();
@@ -2064,7 +1854,6 @@ void wf_finish(const WFParams W) {
       prof_sh++;
 #endif
       const bool sh = st == FS_SHADE;
-#if RT_FINISH_RELOAD
       // the shade step reads its parameters through an opaque copy of the kernel-argument address,
       // so their ~30 pointers are loaded here (scalar loads) instead of being held in SGPRs
       // across the trace loop
@@ -2076,10 +1865,6 @@ void wf_finish(const WFParams W) {
       const Env EL{PL.hdr, PL.cache, PL.light, PL.hdr_w, PL.hdr_h, PL.hdr_res, PL.env_angle, PL.env_intensity};
       unsigned long long ns = 0;  // (a coop group runs its path's shade step on all its lanes: counted once)
       const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, ns);
-#else
-      unsigned long long ns = 0;
-      const ShadeOut o = shade_path<BSDF, true>(W, E, path, sh, false, true, ns);
-#endif
       if (lead()) nsamples += ns;
       if (sh) {
         if (lead()) nsteps++;

@@ -26,7 +26,7 @@ RT_FLAG_NO_FINISH = 8
 RT_FLAG_FINISH = 16
 RT_FLAG_SERIAL = 32
 RT_FLAG_SORTED_TRAVERSAL = 64
-RT_ABI_VERSION = 4
+RT_ABI_VERSION = 5
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 
 _f32p = C.POINTER(C.c_float)
@@ -371,9 +371,8 @@ class Renderer:
     def render(self, params: FrameParams, rand_origins: Sequence[float]) -> dict:
         ro = np.ascontiguousarray(rand_origins, np.float32)
         p = params.to_c()
-        st = RtStats()
-        self._check(self._L.rt_render(self._h, C.byref(p), _fp(ro), len(ro), C.byref(st)), "rt_render")
-        return st.as_dict()
+        self._check(self._L.rt_render(self._h, C.byref(p), _fp(ro), len(ro), None), "rt_render")
+        return self.stats()  # rt_render's own snapshot holds only the ABI-3 fields
 
     def synchronize(self) -> None:
         self._check(self._L.rt_synchronize(self._h), "rt_synchronize")

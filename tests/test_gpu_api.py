@@ -357,3 +357,62 @@ def test_thousands_of_calls_without_synchronize(gpu_renderer, env_maps, depth):
     assert bit_mismatch(r.read_accum(), ref)[0] == 0.0
     assert st2["rays"] == st["rays"]
     assert st2["launches"] == n
+    # the traversal launches' busy union (folded in bounded memory: intervals of calls <= k-2 are
+    # summed and dropped) lies within the calls' summed time and is not empty
+    assert 0.0 < st2["trace_busy_ms"] <= st2["kernel_ms"] * 1.001, st2
+
+
+def test_bench_operating_point_matches_oracle(gpu_renderer, env_maps):
+    """bench.py's operating point, pinned against the oracle.  The bench renders
+    C3 in 1024-frame calls at loopNum 1 .. 25,600 (5 warm-up + 20 timed steps), each call two
+    launches of 512 frames (the path-state budget), each launch two frame groups of 256 frames
+    traced by the bulk kernels (groups of 530 M slots, far above the finisher's limit).  Here the
+    same shape at 48x27: one call of 1024 frames at loopNum 24,001 .. 25,024 (randOrigin from the
+    same glibc sequence, Sobol indices loopNum + 1 up to 25,025, RT:616-620), a budget of 512
+    frames (two launches), the finisher's slot limit at 1 (every group on the bulk kernels), over a
+    host-written history as if 24,000 frames were accumulated (the blend weights {1/n, (n-1)/n}
+    at n ~ 25 k, RT:1552).  Image bit for bit and the device ray count equal the oracle's."""
+    sd = cf.config_scene("C3")
+    W, H = 48, 27
+    first, n = 24001, 1024
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, first, n, ro_offset=first - 1)
+    hist = np.random.default_rng(5).uniform(0.0, 2.0, (H, W, 3)).astype(np.float32)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames, accum=hist)
+    r = gpu_renderer
+    r.set_max_paths(512 * W * H)
+    r.set_finish(2, 1)
+    try:
+        img, st = gpu_render(r, sd, env_maps, W, H, fp, ro, accum=hist, loop_num=first - 1)
+    finally:
+        r.set_max_paths(0)
+        r.set_finish(2, 8 << 20)
+    assert r.loop_num == first + n - 1
+    assert st["launches"] == 2 and st["trace_launches"] == 2 * 2 * 9, st  # batches x groups x passes
+    assert st["finish_steps"] == 0 and st["samples"] == W * H * n
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_stats_get_writes_the_abi3_struct_only(gpu_renderer, env_maps):
+    """ABI 5: rt_stats_get (and rt_render's stats argument) write the 104 bytes of the ABI-3 rt_stats
+    a binding of that header allocated, never the fields added since; rt_stats_get_sized with the
+    full size returns those."""
+    import ctypes as C
+    from rtamd.renderer import RtStats
+    sd = cf.config_scene("C2")
+    W, H = 32, 32
+    fp = cf.frame_params(W, H)
+    ro, _ = frames_for(fp, 1, 2)
+    gpu_render(gpu_renderer, sd, env_maps, W, H, fp, ro)
+    L, h = gpu_renderer._L, gpu_renderer._h
+    buf = (C.c_uint8 * 256)(*([0xAB] * 256))
+    assert L.rt_stats_get(h, C.cast(buf, C.POINTER(RtStats))) == 0
+    assert all(b == 0xAB for b in bytes(buf)[104:]), "rt_stats_get wrote past the ABI-3 struct"
+    full = gpu_renderer.stats()
+    assert int.from_bytes(bytes(buf)[0:8], "little") == full["rays"] > 0
+    assert full["pass0_steps"] > 0 and full["trace_busy_ms"] > 0.0
+    buf2 = (C.c_uint8 * 256)(*([0xAB] * 256))
+    p = C.cast(buf2, C.POINTER(RtStats))
+    assert L.rt_render(h, C.byref(fp.to_c()), ro.ctypes.data_as(C.POINTER(C.c_float)), 1, p) == 0
+    assert all(b == 0xAB for b in bytes(buf2)[104:]), "rt_render wrote past the ABI-3 struct"

@@ -6,9 +6,7 @@ near-first traversal.  With the derived bound (cull_eps, rt_render.hip cull_boun
 image equals the oracle bit for bit; with the bound's eps term forced to 0
 (RT_CULL_EPS_SCALE=0, the round-1 margin; a switch only lib/librtamd_dev.so reads) the GPU culls
 T's box and returns the wall: the test also checks that this failure shows, so it really
-exercises the hole.  The hole needs the near-first child order (the wall's box entered before
-T's), so that render asks for it with RT_FLAG_SORTED_TRAVERSAL: the octant-ordered fast traversal
-may visit T's box first on this scene and then keep T whatever the margin.
+exercises the hole (the near-first child order enters the wall's box before T's).
 """
 import numpy as np
 import pytest
@@ -16,7 +14,7 @@ import pytest
 from cull_cases import old_margin_counterexample
 from helpers import bit_mismatch
 from rtamd import configs as cf
-from rtamd.renderer import RT_FLAG_MEGAKERNEL, RT_FLAG_SORTED_TRAVERSAL
+from rtamd.renderer import RT_FLAG_MEGAKERNEL
 from test_cull_bound import cull_frame_params
 
 pytestmark = pytest.mark.gpu
@@ -47,10 +45,6 @@ def test_culling_keeps_the_reference_hit(gpu_renderer, gpu_dev_renderer, env_map
     monkeypatch.setenv("RT_CULL_EPS_SCALE", "0")
     same, _, _, _ = _render_both(gpu_renderer, env_maps, c, fp)
     assert bit_mismatch(same, ref)[0] == 0.0, "the release library must ignore RT_CULL_EPS_SCALE"
-    sorted_fp = cull_frame_params(c)
-    sorted_fp.flags = flags | RT_FLAG_SORTED_TRAVERSAL
-    exact, _, _, _ = _render_both(gpu_renderer, env_maps, c, sorted_fp)
-    assert bit_mismatch(exact, ref)[0] == 0.0
-    bad, _, _, _ = _render_both(gpu_dev_renderer, env_maps, c, sorted_fp)
+    bad, _, _, _ = _render_both(gpu_dev_renderer, env_maps, c, fp)
     assert bit_mismatch(bad, ref)[0] > 0.5, "the round-1 margin should lose T on this scene"
     assert np.all(bad[..., 1] > bad[..., 0]), "with the round-1 margin the green wall wins"

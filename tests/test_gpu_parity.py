@@ -11,13 +11,13 @@ import pytest
 
 from helpers import bit_mismatch, frames_for, gpu_render, oracle_render
 from rtamd import configs as cf
+from rtamd import scene_lib as sl
 from rtamd.renderer import RT_FLAG_MEGAKERNEL, RT_FLAG_NO_CULL, RT_FLAG_SORTED_TRAVERSAL
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("flags", [0, RT_FLAG_SORTED_TRAVERSAL, RT_FLAG_MEGAKERNEL],
-                         ids=["wavefront", "wavefront-sorted", "megakernel"])
+@pytest.mark.parametrize("flags", [0, RT_FLAG_MEGAKERNEL], ids=["wavefront", "megakernel"])
 @pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
 def test_config_matches_oracle_bitwise(gpu_renderer, env_maps, name, flags):
     sd = cf.config_scene(name)
@@ -213,3 +213,69 @@ def test_lane_quads_move_overflow_stacks(gpu_dev_renderer, env_maps, monkeypatch
     img, st = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def _level_camera(W, H, yaw=-90.0):
+    """The default camera turned level (pitch 0, Camera.h:160-174): Front.y = sin(0) = 0, so Right.y
+    = 0 and Up = (0, u, 0), and the camera ray of every pixel of the middle row of an odd height
+    (v = 0.5: LBC.y = -halfH*Up.y, plus (0.5*2*halfH)*Up.y) has a y component of exactly 0."""
+    cam = sl.camera(yaw, 0.0, cf.CAMERA_ZOOM, float(np.float32(W) / np.float32(H)))
+    return cf.frame_params(W, H, front=cam["front"], right=cam["right"], up=cam["up"],
+                           left_bottom_corner=cam["left_bottom_corner"], half_h=cam["half_h"],
+                           half_w=cam["half_w"])
+
+
+def _camera_dirs(fp, W, H):
+    """wf_camera's operations (RT:1527 before normalize, fp32, left to right): the unnormalised
+    camera directions, (H, W, 3); a zero component stays zero through normalize."""
+    f = np.float32
+    px, py = np.meshgrid(np.arange(W, dtype=f), np.arange(H, dtype=f))
+    u = (px + f(0.5)) / f(W)
+    v = (py + f(0.5)) / f(H)
+    a = (u * f(2.0)) * f(fp.half_w)
+    b = (v * f(2.0)) * f(fp.half_h)
+    lbc, right, up = (np.asarray(x, f) for x in (fp.left_bottom_corner, fp.right, fp.up))
+    return np.stack([(lbc[k] + a * right[k]) + b * up[k] for k in range(3)], axis=-1)
+
+
+@pytest.mark.parametrize("small", [True, False], ids=["finisher-static", "bulk-kernels"])
+def test_zero_direction_component_rays_match_oracle(gpu_renderer, env_maps, small):
+    """Rays with an exactly zero direction component take the literal slab of RT:309-310 (1/d =
+    +-inf; tl_qnode_keys / coop_box).  Its per-axis min / max turns a QNode's empty slot (the
+    inverted box lo = +inf, hi = -inf) into an infinite box, so that path must test the slot's ref:
+    round 4 (ccd9513) entered such a slot, i.e. fetched QNode 0x7fffffff (Q_EMPTY), far outside
+    the array — the hipErrorIllegalAddress of gpurun_out/fast1/tests.log.  No other
+    test had such rays (every configuration's camera has pitch -14).  A level camera over C3 gives
+    the middle row of an odd-height frame camera rays with d.y = 0, which cross the dragon's tree
+    (4-wide nodes with fewer than four children sit at every level above its leaves).  Both trace
+    kernel families run it: the one-frame / small-pass kernels with the finisher's lane quads, and
+    the bulk kernels (finisher slot limit 1).  The image and the ray count equal the oracle's."""
+    sd = cf.config_scene("C3")
+    W, H = 64, 37
+    fp = _level_camera(W, H)
+    d = _camera_dirs(fp, W, H)
+    assert np.all(d[(H - 1) // 2, :, 1] == 0.0) and np.count_nonzero(d[..., 1] == 0.0) == W
+    ro, frames = frames_for(fp, 1, 2)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    r = gpu_renderer
+    if not small:
+        r.set_finish(2, 1)
+    try:
+        img, st = gpu_render(r, sd, env_maps, W, H, fp, ro)
+    finally:
+        r.set_finish(2, 8 << 20)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
+    # the row's camera rays hit the scene (they traverse, not just miss the root box)
+    assert np.any(np.abs(ref[(H - 1) // 2] - ref[0]).sum(axis=-1) > 0)
+
+
+def test_sorted_traversal_flag_is_accepted(gpu_renderer, env_maps):
+    """RT_FLAG_SORTED_TRAVERSAL (ABI 4) has no effect since ABI 5 (the octant-ordered traversal it
+    switched off was removed): a call with it renders the same image as one without."""
+    sd = cf.config_scene("C3")
+    W, H = 48, 32
+    ro, frames = frames_for(cf.frame_params(W, H), 1, 1)
+    a, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, cf.frame_params(W, H), ro)
+    b, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, cf.frame_params(W, H, flags=RT_FLAG_SORTED_TRAVERSAL), ro)
+    assert bit_mismatch(a, b)[0] == 0.0
