@@ -296,6 +296,10 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
 // before finishing the first, and idle lanes refill from the queue.  (Measured and removed: the
 // if-if schedule, while-while and Aila & Laine's speculative while-while)
 
+#ifndef RT_CACHED_LIMIT  // the culling limit kept per ray (1 VGPR) instead of recomputed at every use: C3 bulk
+                         // +0.58% (round 5, profiles/r05_ab_bulk_cached_limit_C3.log; round 2's attempt spilled)
+#define RT_CACHED_LIMIT 1
+#endif
 struct TraceLane {
   // ray as scalars (f3 members made SROA keep the lane in scratch memory)
   float ox, oy, oz, dx, dy, dz, ix, iy, iz;
@@ -303,7 +307,12 @@ struct TraceLane {
   RTD f3 d() const { return mk3(dx, dy, dz); }
   RTD f3 inv() const { return mk3(ix, iy, iz); }
   float best, bestt;
-  RTD float limit(float eps) const { return cull_limit(best, eps, ix, iy, iz); }
+  float lim;  // RT_CACHED_LIMIT: cull_limit of the current best, updated when best changes
+  RTD float limit(float eps) const { return RT_CACHED_LIMIT ? lim : cull_limit(best, eps, ix, iy, iz); }
+  RTD void set_best(float d, float eps) {
+    best = d;
+    if (RT_CACHED_LIMIT) lim = cull_limit(d, eps, ix, iy, iz);
+  }
   int besttri, sp, cur, tri_i, tri_end;
   int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
   bool haveCur, anyhit, finite;
@@ -443,7 +452,7 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   ok &= inside;
   if (WIDE && ok && dist == L.best) ok = L.besttri >= 0 && tie_wins(P, L, i, L.besttri);
   if (ok) {
-    L.best = dist;
+    L.set_best(dist, P.cull_eps);
     L.besttri = i;
     L.bestt = t;
   }
@@ -660,7 +669,7 @@ RTD void tl_start(const KParams& P, TraceLane& L) {
   L.offNx = (L.ix > 0.0f || !L.finite) ? 0 : 48;
   L.offNy = (L.iy > 0.0f || !L.finite) ? 16 : 64;
   L.offNz = (L.iz > 0.0f || !L.finite) ? 32 : 80;
-  L.best = INF;
+  L.set_best(INF, P.cull_eps);
   L.besttri = -1;
   L.bestt = 0.0f;
   L.sp = 0;
@@ -855,7 +864,7 @@ RTD bool tl_tri_coop(const KParams& P, TraceLane& L, int c) {
     if (finished || !hq || dq > L.best) return;
     const int iq = L.tri_i + q;
     if (dq == L.best && !(L.besttri >= 0 && tie_wins(P, L, iq, L.besttri))) return;
-    L.best = dq;
+    L.set_best(dq, P.cull_eps);
     L.besttri = iq;
     L.bestt = tq;
     if (L.anyhit) {
@@ -923,6 +932,7 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
   L.dx = __shfl(L.dx, src); L.dy = __shfl(L.dy, src); L.dz = __shfl(L.dz, src);
   L.ix = __shfl(L.ix, src); L.iy = __shfl(L.iy, src); L.iz = __shfl(L.iz, src);
   L.best = __shfl(L.best, src); L.bestt = __shfl(L.bestt, src); L.besttri = __shfl(L.besttri, src);
+  if (RT_CACHED_LIMIT) L.lim = __shfl(L.lim, src);
   L.sp = sp_src; L.cur = __shfl(L.cur, src);
   L.tri_i = __shfl(L.tri_i, src); L.tri_end = __shfl(L.tri_end, src);
   L.offNx = __shfl(L.offNx, src); L.offNy = __shfl(L.offNy, src); L.offNz = __shfl(L.offNz, src);
@@ -1025,7 +1035,7 @@ void wf_trace(const WFParams W) {
   int entry = 0;
   TraceLane L;
   L.ox = L.oy = L.oz = L.dx = L.dy = L.dz = L.ix = L.iy = L.iz = 0.0f;
-  L.best = INF; L.bestt = 0.0f; L.besttri = -1;
+  L.best = INF; L.bestt = 0.0f; L.besttri = -1; L.lim = INF;
   L.sp = L.cur = L.tri_i = L.tri_end = 0;
   L.haveCur = L.anyhit = false;
   unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_iter = 0;

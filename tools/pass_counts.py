@@ -21,6 +21,7 @@ ap.add_argument("--count", action="store_true", help="RT_FLAG_COUNT_VISITS: step
 ap.add_argument("--lib", default=None, help="library (default lib/librtamd_dev.so)")
 ap.add_argument("--warm", type=int, default=0, help="one-frame calls before the measured one (timelines)")
 ap.add_argument("--order", action="store_true", help="rt_order_work from one probe frame first (as bench.py does)")
+ap.add_argument("--max-paths", type=int, default=0, help="rt_set_max_paths (0: default budget)")
 a = ap.parse_args()
 cfg = cf.CONFIGS[a.config]
 W, H = cfg.width, cfg.height
@@ -29,9 +30,11 @@ r = Renderer(0, lib_path=a.lib or dev_lib_path())
 r.set_scene_soa(sd.soa, sd.nodes)
 r.set_env(*cf.load_env())
 r.resize(W, H)
+if a.max_paths:
+    r.set_max_paths(a.max_paths)
 from rtamd.renderer import RT_FLAG_COUNT_VISITS  # noqa: E402
 fp = cf.frame_params(W, H, flags=RT_FLAG_COUNT_VISITS if a.count else 0)
-ro = cf.rand_origins(8)
+ro = cf.rand_origins(max(8, a.frames))
 if a.order:
     r.order_work(cf.frame_params(W, H), ro[:1])
 for k in range(a.warm):
