@@ -137,24 +137,28 @@ def test_roofline_bound_follows_the_limiter():
     assert r2["avg_launch_ms"] == 16.0 and "co-running" in r2["avg_launch_ms_regime"] and r2["bound"] == "hbm"
 
 
-def _committed_bench_line():
-    """the newest committed bench line in the round-4 roofline format, and its profile"""
-    for p in sorted((ROOT / "profiles").glob("r*_bench_C3.json"), reverse=True):
+def _committed_bench_line(config="C3"):
+    """the newest committed bench line of a configuration in the round-4 roofline format (with a
+    PMC profile), and its profile"""
+    pat = "r*_bench_C3.json" if config == "C3" else f"r*_other_configs/bench_{config}.json"
+    for p in sorted((ROOT / "profiles").glob(pat), reverse=True):
         d = json.loads(p.read_text())
-        if "avg_launch_ms_regime" in d.get("roofline", {}):
+        if "avg_launch_ms_regime" in d.get("roofline", {}) and d["roofline"].get("profile"):
             return p, d
     return None, None
 
 
-def test_committed_roofline_recomputes_from_the_profile():
+@pytest.mark.parametrize("config", ["C3", "C4", "C5"])
+def test_committed_roofline_recomputes_from_the_profile(config):
     """every roofline figure of the committed bench line is recomputable from
     profiles/ and consistent with the step: frac = algorithmic bytes (or VALU instructions) per
     launch / the standalone launch time; the standalone time agrees with rocprof's standalone
     launches within 5%; wf_trace and wf_shade per-launch times x launches per step fit in the step;
     bound = limiter."""
-    p, d = _committed_bench_line()
+    p, d = _committed_bench_line(config)
     if p is None:
-        pytest.skip("no committed round-4 bench line yet")
+        pytest.skip("no committed bench line with a profile yet")
+    assert d["config"]["workload"].startswith(config)
     rf = d["roofline"]
     prof = json.loads((ROOT / rf["profile"]).read_text())
     kt = prof["kernels"]["wf_trace"]
