@@ -252,8 +252,12 @@ RTD f3 camera_ray(const KParams& P, const WFState& S, unsigned int slot, uint32_
 // progressive blend of the frames in flight, in frame order (RT:1552).  Pixel-major slots put
 // a pixel's frames side by side, so the block stages 8 frames of its 256 pixels at a time in LDS
 // with whole-cache-line loads (8 lanes per pixel) and each thread then blends its own pixel.
+// The next stage's loads are issued into registers before the current stage is blended, so the
+// HBM latency overlaps the blend (C3 bulk +0.88%, round 5, profiles/r05_ab_bulk_blend_prefetch_C3.log;
+// the stage's blend weights come through LDS: vector-memory waits are in order, so a weight load
+// issued after the prefetch would wait for it too).
 constexpr int BL_FR = 8, BL_PITCH = BL_FR + 1;  // frames per stage; padded row (bank spread)
-__global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wf_blend(const WFParams W) {
   __shared__ float4 tile[256 * BL_PITCH];
   const KParams& P = W.K;
   const WFState& S = W.S;
@@ -267,20 +271,51 @@ __global__ __launch_bounds__(256) void wf_blend(const WFParams W) {
       const float4 h = P.accum[ai];
       acc = mk3(h.x, h.y, h.z);
     }
-    for (unsigned int f0 = 0; f0 < nf; f0 += BL_FR) {
-      const unsigned int nfc = min((unsigned int)BL_FR, nf - f0);
-      __syncthreads();
-      for (unsigned int i = threadIdx.x; i < 256u * BL_FR; i += 256u) {
-        const unsigned int p = i / BL_FR, k = i % BL_FR;
-        if (base + p < P.n_work && k < nfc) tile[p * BL_PITCH + k] = S.fin[(size_t)(base + p) * nf + f0 + k];
+    {
+      static_assert(BL_FR == 8, "eight named registers");
+      // (unconditional loads from a clamped index: a branch around each load would make the
+      // compiler wait for all of them before the blend below; named registers, not an array:
+      // a loop-carried private array stayed in scratch)
+      float4 r0, r1, r2, r3, r4, r5, r6, r7;
+      __shared__ float2 wst[BL_FR];
+      auto ld1 = [&](unsigned int f0, int j) {
+        const unsigned int nfc = min((unsigned int)BL_FR, nf - f0);
+        const unsigned int i = threadIdx.x + 256u * (unsigned)j, p = i / BL_FR, k = i % BL_FR;
+        const bool ok = base + p < P.n_work && k < nfc;
+        return S.fin[ok ? (size_t)(base + p) * nf + f0 + k : 0];
+      };
+      auto st1 = [&](int j, float4 v) {
+        const unsigned int i = threadIdx.x + 256u * (unsigned)j, p = i / BL_FR, k = i % BL_FR;
+        tile[p * BL_PITCH + k] = v;
+      };
+#define RT_BLEND_FETCH(F0)                                                                          \
+  {                                                                                                 \
+    r0 = ld1(F0, 0); r1 = ld1(F0, 1); r2 = ld1(F0, 2); r3 = ld1(F0, 3);                             \
+    r4 = ld1(F0, 4); r5 = ld1(F0, 5); r6 = ld1(F0, 6); r7 = ld1(F0, 7);                             \
+  }
+      RT_BLEND_FETCH(0u)
+      for (unsigned int f0 = 0; f0 < nf; f0 += BL_FR) {
+        const unsigned int nfc = min((unsigned int)BL_FR, nf - f0);
+        __syncthreads();
+        st1(0, r0); st1(1, r1); st1(2, r2); st1(3, r3); st1(4, r4); st1(5, r5); st1(6, r6); st1(7, r7);
+        // (read from LDS after the barrier: a vector-memory load of them after the prefetch below
+        // would wait for the prefetch too, vmcnt being in order)
+        if (threadIdx.x < (unsigned)BL_FR) wst[threadIdx.x] = P.blend_w[f0 + (threadIdx.x < nfc ? threadIdx.x : 0u)];
+        __syncthreads();
+        float2 bw[BL_FR];  // the stage's blend weights {1 / n, (n - 1) / n}, staged in LDS with the tile
+#pragma unroll
+        for (int k = 0; k < BL_FR; k++) bw[k] = wst[k];
+        if (f0 + BL_FR < nf) RT_BLEND_FETCH(f0 + BL_FR)
+#undef RT_BLEND_FETCH
+        if (valid)
+#pragma unroll
+          for (int k = 0; k < BL_FR; k++) {
+            if ((unsigned)k < nfc) {
+              const float4 c = tile[threadIdx.x * BL_PITCH + k];
+              acc = bw[k].x * xyz(c) + bw[k].y * acc;
+            }
+          }
       }
-      __syncthreads();
-      if (valid)
-        for (unsigned int k = 0; k < nfc; k++) {
-          const float4 c = tile[threadIdx.x * BL_PITCH + k];
-          const float2 bw = P.blend_w[f0 + k];  // {1 / n, (n - 1) / n} (wf_sobol)
-          acc = bw.x * xyz(c) + bw.y * acc;
-        }
     }
     if (valid) P.accum[ai] = make_float4(acc.x, acc.y, acc.z, 0.0f);
   }
