@@ -991,8 +991,9 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
 #endif
-#ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed)
-#define RT_STATIC_FRAC 4
+#ifndef RT_STATIC_FRAC  // eighths of a mid-size pass handed out statically (0: all claimed); C3 1080p one-frame
+                        // calls 5 / 6 / 7 / 8 vs 4: +0.4 / -2.9 / +1.1 / +2.7% (round 5, profiles/r05_ab_single_static_frac_C3.log)
+#define RT_STATIC_FRAC 6
 #endif
 #ifndef RT_TRACE_COOP  // wf_trace (small passes, STATIC): a drained wave with at most this many rays left
                        // moves them to four lanes each (0: off).  C3 1080p one-frame calls, with the
