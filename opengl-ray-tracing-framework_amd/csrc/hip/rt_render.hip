@@ -109,7 +109,10 @@ struct rt_ctx {
     hipEvent_t ev = nullptr;                  // the last upload (the host table is reused after it)
   };
   FrameTable ft[5];
-  int pool_chunk = 1024;                      // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
+#ifndef RT_POOL_CHUNK_DEFAULT
+#define RT_POOL_CHUNK_DEFAULT 1024
+#endif
+  int pool_chunk = RT_POOL_CHUNK_DEFAULT;     // rays per queue atomic in wf_trace (C3: 256 -> 512 -> 1024: +2.3%, +2.4%)
   int2* d_stack_ovf = nullptr;
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;

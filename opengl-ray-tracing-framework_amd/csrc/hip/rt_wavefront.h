@@ -988,6 +988,13 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 #ifndef RT_TAIL_CHUNK  // rays per claim near the end of a pass queue (and per participating wave)
 #define RT_TAIL_CHUNK 64u
 #endif
+#ifndef RT_GUIDED  // bulk passes: claim size = rays left / (waves x RT_GUIDED), between RT_TAIL_CHUNK and the pool
+                   // chunk (0: the pool chunk until the tail, then RT_TAIL_CHUNK).  A late 1024-ray claim of one
+                   // costly pixel run held a wave long after the others had drained.  C3 bulk 1 / 2 / 3 / 4: +0.49 /
+                   // +0.88, +1.04 / +0.32 / -0.07%; N=8 rank shares 70.9 -> 69.9 ms (round 5,
+                   // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep their static shares + 64s
+#define RT_GUIDED 2u
+#endif
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
 #endif
@@ -1094,7 +1101,11 @@ void wf_trace(const WFParams W) {
     // than the lanes it brings back
     if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
       if (pool_next >= pool_end) {
-        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
+        unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
+        if (RT_GUIDED && !STATIC) {  // guided self-scheduling: the rays left (as of this wave's last claim) over the waves x G
+          const unsigned int left = nq - min(pool_end, nq);
+          chunk = min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (part_waves * RT_GUIDED)) & ~63u));
+        }
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
         base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));

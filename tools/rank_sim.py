@@ -51,9 +51,9 @@ costs = r.tile_costs(fp, ro[-a.probe_frames:])
 t1 = None
 modes = ["modulo", "balanced"] if a.assign == "both" else [a.assign]
 for world, mode in [(int(x), m) for x in a.worlds.split(",") for m in modes]:
-    if world == 1 and mode == "balanced":
-        continue
-    owner = tiling.balance(costs, world) if mode == "balanced" else None
+    if world == 1 and mode == "balanced" and "modulo" in modes:
+        continue  # (one rank owns every tile either way)
+    owner = tiling.balance(costs, world) if mode == "balanced" and world > 1 else None
     times, rays = [], []
     for rank in range(world):
         r.resize(W, H, tile=a.tile, rank=rank, world=world)
