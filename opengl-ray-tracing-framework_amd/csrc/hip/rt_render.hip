@@ -845,7 +845,7 @@ int alloc_wavefront(rt_ctx* c, size_t paths) {
     w.fin = (float4*)carve(P * 16);
     w.queue[0] = (int*)carve(P * 8); w.queue[1] = (int*)carve(P * 8);
     w.active[0] = (int*)carve(P * 4); w.active[1] = (int*)carve(P * 4);
-    w.cnt = (unsigned int*)carve(64);
+    w.cnt = (unsigned int*)carve(rtd::kCntWords * 4);
   }
   c->wf_paths = P;
   return RT_OK;

@@ -71,6 +71,11 @@ struct WFState {
   unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
 };
 
+// WFState::cnt word of the bulk trace's claim counter of queue segment s (RT_XCD_CLAIMS): one 128-B
+// line each, after the 16 pass counters
+RTD constexpr unsigned int xcnt(unsigned int s) { return 32u + 32u * s; }
+constexpr unsigned int kCntWords = 32u + 32u * 8u;
+
 // a ray queued by pass 0 in the 16-B form (see WFState::org): origin and direction
 RTD void p1_ray(const WFState& S, unsigned int n_frames, unsigned int path, const float4 a, float& ox, float& oy,
                 float& oz) {
@@ -178,6 +183,8 @@ __global__ __launch_bounds__(256) void wf_camera(const WFParams W, const GroupCo
   const KParams& P = W.K;
   const WFState& S = W.S;
   if (blockIdx.x == 0 && threadIdx.x < 16u * (unsigned)Z.n) Z.cnt[threadIdx.x >> 4][threadIdx.x & 15u] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x >= 64u && threadIdx.x < 64u + 8u * (unsigned)Z.n)  // the segment counters
+    Z.cnt[(threadIdx.x - 64u) >> 3][xcnt((threadIdx.x - 64u) & 7u)] = 0u;
   const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
   const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
   const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
@@ -988,12 +995,18 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
 #ifndef RT_TAIL_CHUNK  // rays per claim near the end of a pass queue (and per participating wave)
 #define RT_TAIL_CHUNK 64u
 #endif
-#ifndef RT_GUIDED  // bulk passes: claim size = rays left / (waves x RT_GUIDED), between RT_TAIL_CHUNK and the pool
-                   // chunk (0: the pool chunk until the tail, then RT_TAIL_CHUNK).  A late 1024-ray claim of one
-                   // costly pixel run held a wave long after the others had drained.  C3 bulk 1 / 2 / 3 / 4: +0.49 /
-                   // +0.88, +1.04 / +0.32 / -0.07%; N=8 rank shares 70.9 -> 69.9 ms (round 5,
-                   // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep their static shares + 64s
+#ifndef RT_GUIDED  // bulk passes: claim size = rays left in the segment (as of the wave's last claim there) / (its
+                   // waves x RT_GUIDED), between RT_TAIL_CHUNK and the pool chunk (before: the pool chunk until
+                   // the last grid lanes x RT_TAIL_FACTOR rays, then RT_TAIL_CHUNK).  A late 1024-ray claim of one
+                   // costly pixel run held a wave long after the others had drained.  With one counter, C3 bulk
+                   // 1 / 2 / 3 / 4: +0.49 / +0.88, +1.04 / +0.32 / -0.07%; N=8 rank shares 70.9 -> 69.9 ms (round 5,
+                   // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep static shares + 64-ray claims
 #define RT_GUIDED 2u
+#endif
+#ifndef RT_XCD_CLAIMS  // bulk passes: 8 queue segments with a claim counter each (below).  C3 bulk -0.13% (noise);
+                       // N=8 rank shares: slowest rank 70.1 / 70.4 -> 69.4 / 69.7 ms (round 5,
+                       // profiles/r05_ab_bulk_segment_claims_C3.log, profiles/r05_rank_sim_segment_claims/)
+#define RT_XCD_CLAIMS 1
 #endif
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
@@ -1074,6 +1087,11 @@ void wf_trace(const WFParams W) {
     pool_next = wave_id * static_per;
     pool_end = pool_next + static_per;
   }
+  // RT_XCD_CLAIMS: the bulk pass's queue in 8 segments, each claimed through its own counter
+  // (S.cnt[xcnt(s)], a cache line each); a wave starts on segment blockIdx % 8 (its XCD) and
+  // moves on when a segment is exhausted, drained after 8 empty segments
+  unsigned int seg = blockIdx.x & 7u, seg_tries = 0, seg_seen = 0;
+  const unsigned int seg_waves = max(1u, part_waves / 8u);
   const int lane = (int)(threadIdx.x & 63);
   int entry = 0;
   TraceLane L;
@@ -1091,21 +1109,40 @@ void wf_trace(const WFParams W) {
 
   while (true) {
     if (COUNT) v_iter++;
-    // ---- refill idle lanes from the wave's pool.  One counter serves the whole chip and a
-    // single atomic address sustains only ~90 atomics/us, so the pool is claimed in big chunks
-    // (P.pool_chunk rays per atomic) while plenty of rays remain, in 64s near the end of the
-    // queue so the last rays still spread over all waves.
+    // ---- refill idle lanes from the wave's pool.  A single atomic address sustains only ~90
+    // atomics/us, so the pool is claimed in big chunks (P.pool_chunk rays per atomic) while plenty
+    // of rays remain and in smaller ones towards the end, so the last rays still spread over all
+    // waves: in the bulk passes from 8 queue segments by guided self-scheduling (RT_XCD_CLAIMS,
+    // RT_GUIDED), in the small passes after their static shares in 64s near the end of the queue.
     const unsigned long long idle = __ballot(!busy);
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
     if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
-      if (pool_next >= pool_end) {
-        unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
-        if (RT_GUIDED && !STATIC) {  // guided self-scheduling: the rays left (as of this wave's last claim) over the waves x G
-          const unsigned int left = nq - min(pool_end, nq);
-          chunk = min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (part_waves * RT_GUIDED)) & ~63u));
+      if (RT_XCD_CLAIMS && !STATIC && pool_next >= pool_end) {
+        while (true) {  // (wave-uniform)
+          const unsigned int lo = (unsigned int)((unsigned long long)nq * seg / 8u);
+          const unsigned int hi = (unsigned int)((unsigned long long)nq * (seg + 1u) / 8u);
+          const unsigned int left = hi - min(max(seg_seen, lo), hi);
+          const unsigned int chunk = min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (seg_waves * RT_GUIDED)) & ~63u));
+          unsigned int b = 0;
+          if (lane == 0) b = atomicAdd(&S.cnt[xcnt(seg)], chunk);
+          b = lo + __builtin_amdgcn_readfirstlane(__shfl(b, 0));
+          if (b < hi) {
+            pool_next = b;
+            pool_end = min(b + chunk, hi);
+            seg_seen = pool_end;
+            break;
+          }
+          if (++seg_tries >= 8u) {
+            drained = true;
+            break;
+          }
+          seg = (seg + 1u) & 7u;
+          seg_seen = 0;
         }
+      } else if (pool_next >= pool_end) {
+        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
         base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
@@ -1652,6 +1689,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
     }
   }
+  if (RT_XCD_CLAIMS && blockIdx.x == 0 && threadIdx.x < 8u) S.cnt[xcnt(threadIdx.x)] = 0u;  // (the same, per segment)
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
