@@ -874,8 +874,8 @@ int rt_create(int hip_device, rt_ctx** out) {
   if (const char* e = knob("RT_FINISH_PASS")) c->finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_PIPE_FINISH_PASS")) c->pipe_finish_pass = std::max(0, atoi(e));
   if (const char* e = knob("RT_FINISH_SLOTS")) c->finish_slots = (uint64_t)strtoull(e, nullptr, 10);
-  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, 128 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMalloc(&c->d_counter, 64) != hipSuccess || hipMalloc(&c->d_stats, rtd::kStatWords * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, rtd::kStatWords * sizeof(unsigned long long)) != hipSuccess) {
     rt_destroy(c);
     return RT_ERR_HIP;
   }
@@ -1889,22 +1889,26 @@ int stats_fill(rt_ctx* c, rt_stats* st) {
   int rc = rt_synchronize(c);
   if (rc) return rc;
   memset(st, 0, sizeof(*st));
-  unsigned long long h[8];
-  HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-  st->rays = h[0]; st->samples = h[1]; st->internal_pops = h[2]; st->leaf_pops = h[3]; st->tri_tests = h[4];
+  std::vector<unsigned long long> all(rtd::kStatWords);
+  HIPCHK(c, hipMemcpy(all.data(), c->d_stats, all.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  const unsigned long long* h = all.data();
+  unsigned long long shard[3] = {0, 0, 0};  // the per-wave flushes' shard lines (rays, samples, finish steps)
+  for (unsigned int s = 0; s < rtd::kStatShards; s++)
+    for (int k = 0; k < 3; k++) shard[k] += h[rtd::stats_shard(s) + k];
+  st->rays = h[0] + shard[0]; st->samples = h[1] + shard[1];
+  st->internal_pops = h[2]; st->leaf_pops = h[3]; st->tri_tests = h[4];
   st->launches = c->launches;
   st->kernel_ms = c->kernel_ms;
   st->trace_launches = c->trace_launches;
   st->trace_ms = c->trace_ms;
   st->trace_iters = h[5];
   st->trace_iters_max = h[6];
-  unsigned long long ps[5] = {0, 0, 0, 0, 0};
-  HIPCHK(c, hipMemcpy(ps, c->d_stats + 16, sizeof(ps), hipMemcpyDeviceToHost));
+  const unsigned long long* ps = h + 16;
   st->path_steps = ps[0];
   st->p1_rays = ps[1];
   st->pass0_steps = ps[2];
   st->pass1_steps = ps[3];
-  st->finish_steps = ps[4];
+  st->finish_steps = ps[4] + shard[2];
   double busy = c->busy_closed_ms;
   for (const auto& iv : c->busy) busy += iv.hi - iv.lo;
   st->trace_busy_ms = busy;
@@ -1915,7 +1919,7 @@ int rt_stats_reset(rt_ctx* c) {
   if (!c) return RT_ERR_ARG;
   int rc = rt_synchronize(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long)));
+  HIPCHK(c, hipMemset(c->d_stats, 0, rtd::kStatWords * sizeof(unsigned long long)));
   c->kernel_ms = 0.0;
   c->launches = 0;
   c->trace_ms = 0.0;

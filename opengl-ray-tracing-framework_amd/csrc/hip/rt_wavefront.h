@@ -76,6 +76,17 @@ struct WFState {
 RTD constexpr unsigned int xcnt(unsigned int s) { return 32u + 32u * s; }
 constexpr unsigned int kCntWords = 32u + 32u * 8u;
 
+// Per-wave statistics flushes of wf_shade / wf_finish (rays, samples, finisher steps): with
+// RT_STATS_SHARDS they go to one of kStatShards 128-B lines after the 128 counters (words 0, 1,
+// 2 of shard s = rays, samples, finish steps), summed by the host, instead of all waves of a
+// launch's end queueing at one line: C3 1080p one-frame calls -6.1% (2.488 -> 2.335 ms
+// synchronised), bulk +0.17% (round 5, profiles/r05_ab_stats_shards_C3.log)
+#ifndef RT_STATS_SHARDS
+#define RT_STATS_SHARDS 1
+#endif
+constexpr unsigned int kStatShards = 64u, kStatWords = 128u + 16u * kStatShards;
+__host__ __device__ constexpr unsigned int stats_shard(unsigned int wave) { return 128u + 16u * (wave % kStatShards); }
+
 // a ray queued by pass 0 in the 16-B form (see WFState::org): origin and direction
 RTD void p1_ray(const WFState& S, unsigned int n_frames, unsigned int path, const float4 a, float& ox, float& oy,
                 float& oz) {
@@ -1773,8 +1784,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     nsamples += __shfl_xor(nsamples, off);
   }
   if ((threadIdx.x & 63) == 0 && (nrays | nsamples)) {
-    atomicAdd(&P.stats[0], nrays);
-    atomicAdd(&P.stats[1], nsamples);
+    // (RT_STATS_SHARDS: the launch's last waves all flush at once; spread over shard lines)
+    unsigned long long* st = RT_STATS_SHARDS ? P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6)) : P.stats;
+    atomicAdd(&st[0], nrays);
+    atomicAdd(&st[1], nsamples);
   }
 }
 
@@ -1988,9 +2001,10 @@ void wf_finish(const WFParams W) {
     nsteps += __shfl_xor(nsteps, off);
   }
   if (lane == 0) {
-    atomicAdd(&P.stats[0], nrays);
-    atomicAdd(&P.stats[1], nsamples);
-    atomicAdd(&P.stats[20], nsteps);  // rt_stats.finish_steps
+    unsigned long long* st = RT_STATS_SHARDS ? P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6)) : P.stats;
+    atomicAdd(&st[0], nrays);
+    atomicAdd(&st[1], nsamples);
+    atomicAdd(&st[RT_STATS_SHARDS ? 2 : 20], nsteps);  // rt_stats.finish_steps
   }
 }
 
