@@ -1733,7 +1733,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
             float ms = 0.0f;
             HIPCHK(c, hipEventElapsedTime(&ms, t0, t1));
             HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-            HIPCHK(c, hipMemcpy(q, WP.S.cnt + (pass & 1), 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(q, WP.S.cnt + rtd::cq(pass & 1), 4, hipMemcpyDeviceToHost));
             fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
                     "wave-iters max %llu ray-steps max %llu\n", g, pass, (WP.cam_n ? WP.cam_n : q[0]), ms, h[2], h[3], h[4], h[5], h[6], h[7]);
             unsigned long long hq[6];

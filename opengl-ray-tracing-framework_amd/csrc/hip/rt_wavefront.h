@@ -68,13 +68,20 @@ struct WFState {
   float4* __restrict__ org;
   int* queue[2];                // ray queue entries: path << 1 | is_shadow
   int* active[2];               // active path ids
-  unsigned int* __restrict__ cnt;  // [0..1] queue counts, [2..3] active counts, [4] trace fetch
+  unsigned int* __restrict__ cnt;  // queue counts, active counts, trace fetch, segment claims (cq, ca, ... below)
 };
 
-// WFState::cnt word of the bulk trace's claim counter of queue segment s (RT_XCD_CLAIMS): one 128-B
-// line each, after the 16 pass counters
-RTD constexpr unsigned int xcnt(unsigned int s) { return 32u + 32u * s; }
-constexpr unsigned int kCntWords = 32u + 32u * 8u;
+// WFState::cnt words: the ray-queue counts of the two pass parities (cq), the active-list counts
+// (ca), the trace's / finisher's fetch counter and the claim counters of the 8 queue segments
+// (xcnt, RT_XCD_CLAIMS), one 128-B line each: a device-scope atomic occupies its line ~11 ns (88
+// per us per line, whatever the word, and lines scale: tools/atomic_bench.hip,
+// profiles/r05_atomic_throughput.log).  (The pass counters on lines of their own measured
+// neutral, round 5.)
+__host__ __device__ constexpr unsigned int cq(unsigned int i) { return i; }
+__host__ __device__ constexpr unsigned int ca(unsigned int i) { return 2u + i; }
+constexpr unsigned int kCntFetch = 4u;
+__host__ __device__ constexpr unsigned int xcnt(unsigned int s) { return 160u + 32u * s; }
+constexpr unsigned int kCntWords = 160u + 32u * 8u;
 
 // Per-wave statistics flushes of wf_shade / wf_finish (rays, samples, finisher steps): with
 // RT_STATS_SHARDS they go to one of kStatShards 128-B lines after the 128 counters (words 0, 1,
@@ -193,9 +200,8 @@ struct GroupCounters {
 __global__ __launch_bounds__(256) void wf_camera(const WFParams W, const GroupCounters Z) {
   const KParams& P = W.K;
   const WFState& S = W.S;
-  if (blockIdx.x == 0 && threadIdx.x < 16u * (unsigned)Z.n) Z.cnt[threadIdx.x >> 4][threadIdx.x & 15u] = 0u;
-  if (blockIdx.x == 0 && threadIdx.x >= 64u && threadIdx.x < 64u + 8u * (unsigned)Z.n)  // the segment counters
-    Z.cnt[(threadIdx.x - 64u) >> 3][xcnt((threadIdx.x - 64u) & 7u)] = 0u;
+  if (blockIdx.x == 0)
+    for (unsigned int i = threadIdx.x; i < kCntWords * (unsigned)Z.n; i += blockDim.x) Z.cnt[i / kCntWords][i % kCntWords] = 0u;
   const f3 lbc = mk3(P.lbc[0], P.lbc[1], P.lbc[2]);
   const f3 right = mk3(P.right[0], P.right[1], P.right[2]);
   const f3 up = mk3(P.up[0], P.up[1], P.up[2]);
@@ -1014,6 +1020,10 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep static shares + 64-ray claims
 #define RT_GUIDED 2u
 #endif
+#ifndef RT_STATIC_SEG_CLAIMS  // the small passes' dynamic claims from the 8 segments too: C3 1080p one-frame calls
+                              // -1.3% (round 5, profiles/r05_ab_single_segment_claims_C3.log)
+#define RT_STATIC_SEG_CLAIMS 1
+#endif
 #ifndef RT_XCD_CLAIMS  // bulk passes: 8 queue segments with a claim counter each (below).  C3 bulk -0.13% (noise);
                        // N=8 rank shares: slowest rank 70.1 / 70.4 -> 69.4 / 69.7 ms (round 5,
                        // profiles/r05_ab_bulk_segment_claims_C3.log, profiles/r05_rank_sim_segment_claims/)
@@ -1051,10 +1061,10 @@ void wf_trace(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int qin = W.pass & 1;
-  const unsigned int nq = CAM ? W.cam_n : S.cnt[qin];
+  const unsigned int nq = CAM ? W.cam_n : S.cnt[cq(qin)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
-    S.cnt[qin ^ 1] = 0u;
-    S.cnt[2 + (qin ^ 1)] = 0u;
+    S.cnt[cq(qin ^ 1)] = 0u;
+    S.cnt[ca(qin ^ 1)] = 0u;
   }
   if (nq == 0u || !P.has_scene) {
     if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
@@ -1130,12 +1140,15 @@ void wf_trace(const WFParams W) {
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
     if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
-      if (RT_XCD_CLAIMS && !STATIC && pool_next >= pool_end) {
+      if (RT_XCD_CLAIMS && (!STATIC || RT_STATIC_SEG_CLAIMS) && pool_next >= pool_end) {
         while (true) {  // (wave-uniform)
-          const unsigned int lo = (unsigned int)((unsigned long long)nq * seg / 8u);
-          const unsigned int hi = (unsigned int)((unsigned long long)nq * (seg + 1u) / 8u);
+          // (small passes: the segments split what the static shares leave, claimed in 64s)
+          const unsigned int d0 = STATIC ? static_total : 0u, dn = nq - d0;
+          const unsigned int lo = d0 + (unsigned int)((unsigned long long)dn * seg / 8u);
+          const unsigned int hi = d0 + (unsigned int)((unsigned long long)dn * (seg + 1u) / 8u);
           const unsigned int left = hi - min(max(seg_seen, lo), hi);
-          const unsigned int chunk = min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (seg_waves * RT_GUIDED)) & ~63u));
+          const unsigned int chunk = STATIC ? RT_TAIL_CHUNK
+              : min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (seg_waves * RT_GUIDED)) & ~63u));
           unsigned int b = 0;
           if (lane == 0) b = atomicAdd(&S.cnt[xcnt(seg)], chunk);
           b = lo + __builtin_amdgcn_readfirstlane(__shfl(b, 0));
@@ -1155,7 +1168,7 @@ void wf_trace(const WFParams W) {
       } else if (pool_next >= pool_end) {
         const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&S.cnt[4], chunk);
+        if (lane == 0) base = atomicAdd(&S.cnt[kCntFetch], chunk);
         base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= nq) {
           drained = true;
@@ -1691,10 +1704,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
-  const unsigned int na = W.cam_n ? W.cam_n : S.cnt[2 + in];
-  const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[in];
+  const unsigned int na = W.cam_n ? W.cam_n : S.cnt[ca(in)];
+  const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[cq(in)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S.cnt[4] = 0u;  // fetch counter of the next trace pass
+    S.cnt[kCntFetch] = 0u;  // fetch counter of the next trace pass
     if (na) {
       atomicAdd(&P.stats[16], (unsigned long long)na);  // path shade steps (rt_stats.path_steps)
       if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
@@ -1769,8 +1782,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[out], lc[0] + lc[4]) : 0u;
-    lc[3] = lc[1] ? atomicAdd(&S.cnt[2 + out], lc[1]) : 0u;
+    lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[cq(out)], lc[0] + lc[4]) : 0u;
+    lc[3] = lc[1] ? atomicAdd(&S.cnt[ca(out)], lc[1]) : 0u;
   }
   __syncthreads();
   for (unsigned int j = threadIdx.x; j < lc[0] + lc[4]; j += 256u)
@@ -1835,7 +1848,7 @@ void wf_finish(const WFParams W) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1;
-  const unsigned int na = S.cnt[2 + in];
+  const unsigned int na = S.cnt[ca(in)];
   const int lane = (int)(threadIdx.x & 63);
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
@@ -1892,7 +1905,7 @@ void wf_finish(const WFParams W) {
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
       unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(&S.cnt[4], want);
+      if (lane == 0) base = atomicAdd(&S.cnt[kCntFetch], want);
       base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
       const unsigned int idx = base + (unsigned int)__popcll(idle & ((1ull << lane) - 1ull));
 #ifdef RT_FINISH_PROF
