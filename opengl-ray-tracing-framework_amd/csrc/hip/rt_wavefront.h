@@ -1330,8 +1330,14 @@ void wf_trace(const WFParams W) {
 // Paths per block-iteration of wf_shade = 256 x SH_SUB: the block stages its queue / active
 // entries in LDS and claims global space with one atomic per list per block-iteration.
 #ifndef RT_SH_SUB  // C3 on the rebuilt tree: 1 / 2 / 4 / 8 -> -1.2% / 0 / -0.9% / -1.4% (tools/ab_proc.py);
-                   // final build: 3 vs 2 +0.4%
+                   // final build: 3 vs 2 +0.4%; small groups (one frame per call) keep it (4: one-frame calls
+                   // +6.9%, round 4: fewer blocks for their 2 M-path passes)
 #define RT_SH_SUB 3
+#endif
+#ifndef RT_SH_SUB_BULK  // the bulk's shade launches (groups above the finisher's slot budget): round 5, C3
+                        // 2 / 4 vs 3: -1.26 / +0.55%; 4 / 5 / 6 / 7 / 8: +0.40 / +0.74 / +1.02, +1.16 / +1.22 /
+                        // +1.45% (profiles/r05_ab_bulk_shade_sub_C3.log; 10: 149 VGPRs, 3 waves/SIMD)
+#define RT_SH_SUB_BULK 8
 #endif
 constexpr int SH_KEYS = 2;  // 0: no continuation hit (env / end of path); 1: a continuation hit
 
@@ -1346,7 +1352,7 @@ RTD int shade_key(const KParams& P, const WFState& S, int path) {
 #ifndef RT_SHADE_WPE  // 4 waves/SIMD (<= 128 VGPRs, 12 B/lane spill): shade -8% vs the natural 3
 #define RT_SHADE_WPE 4
 #endif
-constexpr int SH_SUB = RT_SH_SUB;
+constexpr int SH_SUB = RT_SH_SUB, SH_SUB_BULK = RT_SH_SUB_BULK;
 
 // One path's shade step (the body of wf_shade, shared with wf_finish): consume the traced results
 // of the current bounce, sample the next one, write the state back and return the rays to queue.
@@ -1694,7 +1700,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
 
 // BSDF: enableBSDF (RT:1369 Disney integrator) or the BRDF integrator (RT:1290), one
 // instantiation each so neither carries the other's registers
-template <bool BSDF, bool FUSE = false>
+template <bool BSDF, bool FUSE = false, int SH_SUB = rtd::SH_SUB>  // SH_SUB: paths per thread and block-iteration
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
   __shared__ int lq[2 * 256 * SH_SUB];
   __shared__ int la[256 * SH_SUB];
