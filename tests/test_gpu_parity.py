@@ -279,3 +279,28 @@ def test_sorted_traversal_flag_is_accepted(gpu_renderer, env_maps):
     a, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, cf.frame_params(W, H), ro)
     b, _ = gpu_render(gpu_renderer, sd, env_maps, W, H, cf.frame_params(W, H, flags=RT_FLAG_SORTED_TRAVERSAL), ro)
     assert bit_mismatch(a, b)[0] == 0.0
+
+
+@pytest.mark.parametrize("small", [True, False], ids=["small-pass-kernels", "bulk-kernels"])
+@pytest.mark.parametrize("W,H,n", [(3, 2, 1), (11, 7, 3), (40, 23, 2)])
+def test_segment_claims_on_tiny_passes(gpu_renderer, env_maps, W, H, n, small):
+    """Round 5: the trace passes claim their rays from 8 queue segments (one counter line each; the
+    small passes after their static shares), and a wave moves on when its segment is exhausted.
+    Passes of 0-7 rays leave segments empty and make every wave walk all 8; frames of 6 to 920
+    pixels, with the bulk kernels (finisher slot limit 1) and the small-pass ones (finisher off so
+    every pass is a wavefront pass): image and ray count equal the oracle's."""
+    from rtamd.renderer import RT_FLAG_NO_FINISH
+    sd = cf.config_scene("C4")  # glass: paths that live to the last bounces
+    fp = cf.frame_params(W, H, flags=0 if not small else RT_FLAG_NO_FINISH)
+    ro, frames = frames_for(fp, 1, n)
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames)
+    r = gpu_renderer
+    if not small:
+        r.set_finish(2, 1)
+    try:
+        img, st = gpu_render(r, sd, env_maps, W, H, fp, ro)
+    finally:
+        r.set_finish(2, 8 << 20)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert st["samples"] == W * H * n
+    assert bit_mismatch(img, ref)[0] == 0.0
