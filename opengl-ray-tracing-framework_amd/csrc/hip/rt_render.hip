@@ -1592,6 +1592,11 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
           if (!e.empty()) return fail(c, RT_ERR_STATE, e);
         }
         WP.K.wave_log = debug_passes ? d_wave_log : nullptr;  // COUNT builds (RT_DEBUG_PASSES)
+#ifdef RT_DEV
+        // RT_DEBUG_WAVES_ONLY: the per-wave timeline without the per-ray step histogram (whose atomics
+        // on a few lines would set the pass times)
+        if (debug_passes && knob("RT_DEBUG_WAVES_ONLY")) WP.K.flags |= rtd::kFlagNoRayHist;
+#endif
         WP.S = c->wfg[set];
         WP.S.pix_xy = c->wf.pix_xy + w0;
         WP.S.pix_acc = c->wf.pix_acc + w0;

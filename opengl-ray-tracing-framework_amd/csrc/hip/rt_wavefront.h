@@ -71,6 +71,8 @@ struct WFState {
   unsigned int* __restrict__ cnt;  // queue counts, active counts, trace fetch, segment claims (cq, ca, ... below)
 };
 
+constexpr int kFlagNoRayHist = 1 << 30;  // (internal, development builds) KParams::flags: no per-ray histogram
+
 // WFState::cnt words: the ray-queue counts of the two pass parities (cq), the active-list counts
 // (ca), the trace's / finisher's fetch counter and the claim counters of the 8 queue segments
 // (xcnt, RT_XCD_CLAIMS), one 128-B line each: a device-scope atomic occupies its line ~11 ns (88
@@ -1036,6 +1038,9 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                         // calls 5 / 6 / 7 / 8 vs 4: +0.4 / -2.9 / +1.1 / +2.7% (round 5, profiles/r05_ab_single_static_frac_C3.log)
 #define RT_STATIC_FRAC 6
 #endif
+#ifndef RT_WAVE_TIMES
+#define RT_WAVE_TIMES 0
+#endif
 #ifndef RT_TRACE_COOP  // wf_trace (small passes, STATIC): a drained wave with at most this many rays left
                        // moves them to four lanes each (0: off).  C3 1080p one-frame calls, with the
                        // finisher's quads: -12.7% back-to-back / -8.6% synchronised against the
@@ -1125,11 +1130,14 @@ void wf_trace(const WFParams W) {
   unsigned long long v_itN = 0, v_itT = 0, v_itO = 0, v_park = 0, v_busyO = 0;  // COUNT: lane utilisation
   unsigned long long v_rays = 0, v_ovf = 0;  // COUNT: rays, overflow-column pushes
   unsigned long long v_q[6] = {0, 0, 0, 0, 0, 0};  // COUNT: node visits by breadth-first index
-  const unsigned long long t_start = COUNT ? wall_clock64() : 0ull;
-  const unsigned long long c_start = COUNT ? clock64() : 0ull;  // shader clock (s_memtime)
+  // RT_WAVE_TIMES (measurement builds): the release kernels log each wave's start / end / iterations
+  // / rays into P.wave_log too (RT_DEBUG_PASSES), as the COUNT kernels do
+  constexpr bool WT = COUNT || RT_WAVE_TIMES;
+  const unsigned long long t_start = WT ? wall_clock64() : 0ull;
+  const unsigned long long c_start = WT ? clock64() : 0ull;  // shader clock (s_memtime)
 
   while (true) {
-    if (COUNT) v_iter++;
+    if (WT) v_iter++;
     // ---- refill idle lanes from the wave's pool.  A single atomic address sustains only ~90
     // atomics/us, so the pool is claimed in big chunks (P.pool_chunk rays per atomic) while plenty
     // of rays remain and in smaller ones towards the end, so the last rays still spread over all
@@ -1274,11 +1282,20 @@ void wf_trace(const WFParams W) {
           atomicAdd(&P.tile_cost[P.cost_blocks ? w >> 6 : S.pix_acc[w] / (unsigned int)(P.tile_w * P.tile_h)],
                     (unsigned long long)(ray_steps + RT_COST_PER_RAY));
         }
-        if (P.wave_log)  // RT_DEBUG_PASSES: steps-per-ray histogram by kind (16-step buckets)
+        if (P.wave_log && !(P.flags & kFlagNoRayHist))  // RT_DEBUG_PASSES: steps-per-ray histogram by kind (16-step buckets)
           atomicAdd(&P.stats[32 + (L.anyhit ? 32 : 0) + (L.besttri >= 0 ? 16 : 0) + min(15u, ray_steps / 16u)], 1ull);
-        ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0; v_rays++;
+        ray_steps_max = max(ray_steps_max, ray_steps); ray_steps = 0;
       }
+      if (WT) v_rays++;
       busy = false;
+    }
+  }
+  if (WT && !COUNT && P.wave_log) {
+    unsigned long long r = v_rays;
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long* w = P.wave_log + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+      w[0] = t_start; w[1] = wall_clock64(); w[2] = v_iter | ((clock64() - c_start) << 20); w[3] = r;
     }
   }
   if (COUNT) {
