@@ -408,8 +408,6 @@ struct TraceStack {
 #endif
     return ovf + (size_t)(j - KL) * ovs + lane();
   }
-  // the lane's current queue entry, kept in LDS after the stack (one VGPR less across the loop)
-  RTD int* entry_slot() const { return reinterpret_cast<int*>(lds0 + KL * TL_LANES) + lane(); }
 };
 
 // byte-offset loads from a uniform base: the compiler emits the saddr form (32-bit lane offset)
