@@ -1024,6 +1024,11 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                               // -1.3% (round 5, profiles/r05_ab_single_segment_claims_C3.log)
 #define RT_STATIC_SEG_CLAIMS 1
 #endif
+#ifndef RT_REFILL_MIN_SMALL  // the small passes' refill threshold: C3 1080p one-frame calls 4 / 6 / 8 / 12 / 16 vs 20:
+                             // -0.5 / -0.7 / -1.1, -0.6 / -0.9, -0.5 / -0.7% back-to-back (round 5,
+                             // profiles/r05_ab_single_refill_min_small_C3.log; the bulk stays at 20)
+#define RT_REFILL_MIN_SMALL 8
+#endif
 #ifndef RT_XCD_CLAIMS  // bulk passes: 8 queue segments with a claim counter each (below).  C3 bulk -0.13% (noise);
                        // N=8 rank shares: slowest rank 70.1 / 70.4 -> 69.4 / 69.7 ms (round 5,
                        // profiles/r05_ab_bulk_segment_claims_C3.log, profiles/r05_rank_sim_segment_claims/)
@@ -1145,7 +1150,7 @@ void wf_trace(const WFParams W) {
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
-    if (idle && !drained && (__popcll(idle) >= RT_REFILL_MIN || idle == __ballot(true))) {
+    if (idle && !drained && (__popcll(idle) >= (STATIC ? RT_REFILL_MIN_SMALL : RT_REFILL_MIN) || idle == __ballot(true))) {
       if (RT_XCD_CLAIMS && (!STATIC || RT_STATIC_SEG_CLAIMS) && pool_next >= pool_end) {
         while (true) {  // (wave-uniform)
           // (small passes: the segments split what the static shares leave, claimed in 64s)
