@@ -183,3 +183,12 @@ def test_cpu_baseline_records_the_host():
     h = bench.host_cpus()
     assert h["nproc"] >= 1 and 1 <= h["affinity"] <= h["nproc"]
     assert "cpu_model" in h
+
+
+def test_bench_tile_default_follows_the_rank_count():
+    """Round 5: 32-px rank tiles at N = 1, 16-px tiles at N > 1 (the cost-balanced map of smaller
+    tiles evens 8 ranks out better); an explicit --tile wins."""
+    import bench
+    assert bench.parse_args([]).tile == 32
+    assert bench.parse_args(["--gpus", "8"]).tile == 16
+    assert bench.parse_args(["--gpus", "2", "--tile", "64"]).tile == 64
