@@ -1381,9 +1381,88 @@ constexpr int SH_SUB = RT_SH_SUB, SH_SUB_BULK = RT_SH_SUB_BULK;
 struct ShadeOut {
   bool qShadow, qCont;
 };
+// The closest hit's geometry (RT:265, RT:1519-1527): t, side, hit point, interpolated normal and
+// material of triangle `tri` on ray (ro, rd) -- tl_triangle_calc's operations on the same ray and
+// triangle.
+struct HitGeom {
+  float t;
+  bool inside;
+  f3 Pp, Ns;
+  int nmat;
+};
+RTD HitGeom hit_geom(const KParams& P, int tri, f3 ro, f3 rd) {
+  const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
+  const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
+  const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
+  const f3 ng = mk3(A.w, B.w, Cc.w);
+  HitGeom h;
+  h.t = (dot(ng, p1) - dot(ro, ng)) / dot(rd, ng);
+  h.inside = dot(ng, rd) > 0.0f;
+  const f3 Pp = ro + rd * h.t;
+  const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
+                      (-(p1.x - p2.x) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
+  const float beta = (-(Pp.x - p3.x) * (p1.y - p3.y) + (Pp.y - p3.y) * (p1.x - p3.x)) /
+                     (-(p2.x - p3.x) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
+  const float gama = 1.0f - alpha - beta;
+  h.Pp = Pp;
+  h.Ns = normalize(alpha * xyz(N1) + beta * xyz(N2) + gama * xyz(N3));
+  h.nmat = __float_as_int(N1.w);
+  return h;
+}
+
+// Camera pass of the bulk groups (RT_CAM_REC): a block-iteration's paths are a few pixels' frames,
+// and every frame of a pixel shades the same camera hit (R6: no jitter).  What depends only on
+// that hit -- geometry, emission, the BSDF frame, or the environment colour of a miss -- is
+// computed once per pixel into LDS (7 float4, kCamRec) by cam_rec and read by the frames' lanes
+// (same functions on the same values: the same bits).  A frame whose own trace result differs
+// from the record's computes everything itself.
+#ifndef RT_CAM_REC
+#define RT_CAM_REC 1
+#endif
+constexpr int kCamRec = 7;
+RTD void cam_rec(const WFParams& W, const Env& E, unsigned int w, float4* rec) {
+  const KParams& P = W.K;
+  const WFState& S = W.S;
+  const unsigned int path0 = w * (unsigned)W.n_frames;  // frame 0 of work item w
+  int r = S.res[2 * path0];
+  const f3 ro = mk3(P.pos[0], P.pos[1], P.pos[2]), rd = xyz(S.cam[w]);
+#ifdef RT_CHECK
+  if (r >= P.n_tri) r = -1;  // (shade_path reports it)
+#endif
+  if (r >= 0) {
+    const HitGeom h = hit_geom(P, r, ro, rd);
+    const f3 hN = h.inside ? -h.Ns : h.Ns;
+    const Mat m = load_mat(P.mats, h.nmat);
+    const BsdfFrame BF = bsdf_frame(m, -rd, hN);
+    const f3 Le0 = xyz(P.mats[8 * h.nmat]);
+    rec[0] = make_float4(h.Pp.x, h.Pp.y, h.Pp.z, h.t - 0.00001f);
+    rec[1] = make_float4(hN.x, hN.y, hN.z, __int_as_float(r));
+    rec[2] = make_float4(Le0.x, Le0.y, Le0.z, __int_as_float(h.nmat));
+    rec[3] = make_float4(BF.eta, BF.T.x, BF.T.y, BF.T.z);
+    rec[4] = make_float4(BF.B.x, BF.B.y, BF.B.z, BF.V.x);
+    rec[5] = make_float4(BF.V.y, BF.V.z, BF.specCol.x, BF.specCol.y);
+    rec[6] = make_float4(BF.specCol.z, BF.sheenCol.x, BF.sheenCol.y, BF.sheenCol.z);
+  } else {
+    const f3 env = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
+    rec[1] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(r));
+    rec[2] = make_float4(env.x, env.y, env.z, 0.0f);
+  }
+}
+RTD BsdfFrame rec_frame(const float4* rec) {
+  const float4 q3 = rec[3], q4 = rec[4], q5 = rec[5], q6 = rec[6];
+  BsdfFrame F;
+  F.eta = q3.x;
+  F.T = mk3(q3.y, q3.z, q3.w);
+  F.B = mk3(q4.x, q4.y, q4.z);
+  F.V = mk3(q4.w, q5.x, q5.y);
+  F.specCol = mk3(q5.z, q5.w, q6.x);
+  F.sheenCol = mk3(q6.y, q6.z, q6.w);
+  return F;
+}
+
 template <bool BSDF, bool FUSE = false>  // FUSE: W.fuse_blend is honoured (one-frame pixel groups)
 RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
-                        unsigned long long& nsamples) {
+                        unsigned long long& nsamples, const float4* rec = nullptr) {
   const KParams& P = W.K;
   const WFState& S = W.S;
   bool doFinish = false, doBounce = false;
@@ -1397,6 +1476,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   f3 hP = splat(0.0f), hN = splat(0.0f), hV = splat(0.0f);
   float hDist = 0.0f;
   int mat = 0;
+  bool useRec = false;  // camera pass: this path's hit is its pixel's record (cam_rec)
   if (live) {
     float4 cam_d = make_float4(0, 0, 0, 0);
     if (camPass) {  // implicit camera pass: the state a camera path starts with
@@ -1425,6 +1505,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       }
     }
     const int rc0 = S.res[2 * path];
+    useRec = camPass && rec != nullptr && __float_as_int(rec[1].w) == rc0;
     float4 oo0, dd0;
     if (camPass) {
       oo0 = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
@@ -1463,7 +1544,21 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       const int r = rc0;
       const float4 oo = oo0, dd = dd0;
       const f3 ro = xyz(oo), rd = xyz(dd);
-      if (r >= 0) {
+      if (useRec && r >= 0) {  // the pixel's camera hit from the record (cam_rec)
+        const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+        Le0 = xyz(q2);
+        hP = xyz(q0);
+        if (W.p1_compact && frame == 0u) S.org[(unsigned)path / (unsigned)W.n_frames] = make_float4(q0.x, q0.y, q0.z, 0.0f);
+        hN = xyz(q1);
+        hV = rd;
+        hDist = q0.w;
+        mat = __float_as_int(q2.w);
+        if (0 < P.max_bounce) doBounce = true;
+        else { fin = Le0 + Lo; doFinish = true; }
+      } else if (useRec) {
+        fin = xyz(rec[2]);
+        doFinish = true;
+      } else if (r >= 0) {
         int tri = r;
 #ifdef RT_CHECK
         if (tri >= P.n_tri) {
@@ -1471,21 +1566,11 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
           tri = 0;
         }
 #endif
-        const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
-        const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
-        const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
-        const f3 ng = mk3(A.w, B.w, Cc.w);
-        // t of the closest hit (RT:265): tl_triangle_calc's operations on the same ray and triangle
-        const float t = (dot(ng, p1) - dot(ro, ng)) / dot(rd, ng);
-        const bool inside = dot(ng, rd) > 0.0f;
-        const f3 Pp = ro + rd * t;
-        const float alpha = (-(Pp.x - p2.x) * (p3.y - p2.y) + (Pp.y - p2.y) * (p3.x - p2.x)) /
-                            (-(p1.x - p2.x) * (p3.y - p2.y) + (p1.y - p2.y) * (p3.x - p2.x) + 1e-7f);
-        const float beta = (-(Pp.x - p3.x) * (p1.y - p3.y) + (Pp.y - p3.y) * (p1.x - p3.x)) /
-                           (-(p2.x - p3.x) * (p1.y - p3.y) + (p2.y - p3.y) * (p1.x - p3.x) + 1e-7f);
-        const float gama = 1.0f - alpha - beta;
-        const f3 Ns = normalize(alpha * xyz(N1) + beta * xyz(N2) + gama * xyz(N3));
-        const int nmat = __float_as_int(N1.w);
+        const HitGeom hg = hit_geom(P, tri, ro, rd);
+        const float t = hg.t;
+        const bool inside = hg.inside;
+        const f3 Pp = hg.Pp, Ns = hg.Ns;
+        const int nmat = hg.nmat;
         if (flags & PF_CAMERA) {  // RT:1541-1544
           Le0 = xyz(P.mats[8 * nmat]);
           Lo = splat(0.0f);
@@ -1605,7 +1690,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   } else if (doBounce) {
     const Mat m = load_mat(P.mats, mat);
     const f3 V = -hV;
-    const BsdfFrame BF = bsdf_frame(m, V, hN);  // shared by the three BSDF calls below
+    const BsdfFrame BF = useRec ? rec_frame(rec) : bsdf_frame(m, V, hN);  // shared by the three BSDF calls below
     // light sample + NEE term (RT:1380-1405), evaluated now, added after the shadow ray
     const float xa = rand_(wseed);  // R24
     const float xb = rand_(wseed);
@@ -1727,9 +1812,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __shared__ int lsort[256 * SH_SUB];  // the block's paths, grouped by shade_key
   __shared__ unsigned int lhist[SH_KEYS], lofs[SH_KEYS];
   __shared__ unsigned int lc[5];  // queue count (shadow rays), active count, queue base, active base, continuations
+  constexpr unsigned int kRecs = 256u * SH_SUB / 64u + 1u;  // pixels a block-iteration spans at >= 64 frames
+  __shared__ float4 lrec[RT_CAM_REC && !FUSE ? kCamRec * kRecs : 1];
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
+  const unsigned int nfr = (unsigned int)W.n_frames;
+  const bool camrec = RT_CAM_REC && !FUSE && W.cam_n && nfr >= 64u;  // (uniform)
   const unsigned int na = W.cam_n ? W.cam_n : S.cnt[ca(in)];
   const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[cq(in)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1767,6 +1856,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       const unsigned int j = (unsigned)sub * 256u + threadIdx.x;
       if (j < nblk) lsort[j] = W.cam_n ? (int)(base + j) : S.active[in][base + j];
     }
+    if (camrec) {  // the block-iteration's pixels' camera hits, one lane each
+      const unsigned int p0 = base / nfr, np = (base + nblk - 1u) / nfr - p0 + 1u;
+      if (threadIdx.x < np) cam_rec(W, E, p0 + threadIdx.x, lrec + kCamRec * threadIdx.x);
+    }
   } else {
   int skey[SH_SUB], srank[SH_SUB], spath[SH_SUB];
 #pragma unroll
@@ -1794,7 +1887,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
-    const ShadeOut so = shade_path<BSDF, FUSE>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples);
+    const float4* rec = camrec ? lrec + kCamRec * ((unsigned)path / nfr - base / nfr) : nullptr;
+    const ShadeOut so = shade_path<BSDF, FUSE>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples, rec);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
     // shadow rays from the front of the block's staging list, continuations from the back: the
     // block's queue run is [shadow rays][continuations], so a trace wave's claim is mostly one
