@@ -332,11 +332,26 @@ RTD f3 SampleGTR1(float rgh, float r1) {  // RT:716-729 (R23: r1 used for both a
   sincos_(phi, &sinPhi, &cosPhi);
   return mk3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
 }
-RTD f3 SampleGGXVNDF(f3 V, float ax, float ay, float r1, float r2) {  // RT:751-769
-  f3 Vh = normalize(mk3(ax * V.x, ay * V.y, V.z));
+// PRE (vt != nullptr): the terms that depend on V and the material only, precomputed by
+// v_terms (camera-hit records, rt_wavefront.h cam_rec): vt[0] = DisneySample's lobe weights,
+// vt[1] = {FV, G1V, GccV, Vh.x}, vt[2] = {Vh.yz, T1.xy}, vt[3] = {T1.z, T2}
+RTD void ggx_vndf_frame(f3 V, float ax, float ay, f3& Vh, f3& T1, f3& T2) {  // RT:753-756
+  Vh = normalize(mk3(ax * V.x, ay * V.y, V.z));
   float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
-  f3 T1 = lensq > 0 ? mk3(-Vh.y, Vh.x, 0) * inversesqrt_(lensq) : mk3(1, 0, 0);
-  f3 T2 = cross(Vh, T1);
+  T1 = lensq > 0 ? mk3(-Vh.y, Vh.x, 0) * inversesqrt_(lensq) : mk3(1, 0, 0);
+  T2 = cross(Vh, T1);
+}
+template <bool PRE = false>
+RTD f3 SampleGGXVNDF(f3 V, float ax, float ay, float r1, float r2, const float4* vt = nullptr) {  // RT:751-769
+  f3 Vh, T1, T2;
+  if constexpr (PRE) {
+    const float4 q1 = vt[1], q2 = vt[2], q3 = vt[3];
+    Vh = mk3(q1.w, q2.x, q2.y);
+    T1 = mk3(q2.z, q2.w, q3.x);
+    T2 = mk3(q3.y, q3.z, q3.w);
+  } else {
+    ggx_vndf_frame(V, ax, ay, Vh, T1, T2);
+  }
   float r = sqrt_(r1);
   float phi = 2.0f * PI * r2;
   float s, c;
@@ -349,11 +364,12 @@ RTD f3 SampleGGXVNDF(f3 V, float ax, float ay, float r1, float r2) {  // RT:751-
   return normalize(mk3(ax * Nh.x, ay * Nh.y, max_(0.0f, Nh.z)));
 }
 
-RTD f3 EvalDiffuse(const Mat& mat, f3 Csheen, f3 V, f3 L, f3 H, float& pdf) {  // RT:925-948
+template <bool PRE = false>
+RTD f3 EvalDiffuse(const Mat& mat, f3 Csheen, f3 V, f3 L, f3 H, float& pdf, const float4* vt = nullptr) {  // RT:925-948
   pdf = 0.0f;
   if (L.z <= 0.0f) return splat(0.0f);
   float FL = SchlickFresnel(L.z);
-  float FV = SchlickFresnel(V.z);
+  float FV = PRE ? vt[1].x : SchlickFresnel(V.z);
   float LH = dot(L, H);
   float FH = SchlickFresnel(LH);
   float Fd90 = 0.5f + 2.0f * LH * LH * mat.roughness;
@@ -365,24 +381,27 @@ RTD f3 EvalDiffuse(const Mat& mat, f3 Csheen, f3 V, f3 L, f3 H, float& pdf) {  /
   pdf = L.z * INV_PI;
   return (1.0f - mat.metallic) * (1.0f - mat.transmission) * (INV_PI * mix_(Fd, ss, mat.subsurface) * mat.baseColor + Fsheen);
 }
-RTD f3 EvalSpecReflection(const Mat& mat, float eta, f3 specCol, f3 V, f3 L, f3 H, float& pdf) {  // RT:950-964
+template <bool PRE = false>
+RTD f3 EvalSpecReflection(const Mat& mat, float eta, f3 specCol, f3 V, f3 L, f3 H, float& pdf,
+                          const float4* vt = nullptr) {  // RT:950-964
   pdf = 0.0f;
   if (L.z <= 0.0f) return splat(0.0f);
   float FM = DisneyFresnel(mat, eta, dot(L, H), dot(V, H));
   f3 F = mix(specCol, splat(1.0f), FM);
   float D = GTR2_Aniso(H.z, H.x, H.y, mat.ax, mat.ay);
-  float G1 = SmithG_GGX_Aniso(fabs_(V.z), V.x, V.y, mat.ax, mat.ay);
+  float G1 = PRE ? vt[1].y : SmithG_GGX_Aniso(fabs_(V.z), V.x, V.y, mat.ax, mat.ay);
   float G2 = G1 * SmithG_GGX_Aniso(fabs_(L.z), L.x, L.y, mat.ax, mat.ay);
   pdf = G1 * D / (4.0f * V.z);
   return F * D * G2 / (4.0f * L.z * V.z);
 }
-RTD f3 EvalSpecRefraction(const Mat& mat, float eta, f3 V, f3 L, f3 H, float& pdf) {  // RT:966-984
+template <bool PRE = false>
+RTD f3 EvalSpecRefraction(const Mat& mat, float eta, f3 V, f3 L, f3 H, float& pdf, const float4* vt = nullptr) {  // RT:966-984
   pdf = 0.0f;
   if (L.z >= 0.0f) return mk3(1.0f, 0.0f, 0.0f);  // R26
   float VH = dot(V, H), LH = dot(L, H);
   float F = DielectricFresnel(fabs_(VH), eta);
   float D = GTR2_Aniso(H.z, H.x, H.y, mat.ax, mat.ay);
-  float G1 = SmithG_GGX_Aniso(fabs_(V.z), V.x, V.y, mat.ax, mat.ay);
+  float G1 = PRE ? vt[1].y : SmithG_GGX_Aniso(fabs_(V.z), V.x, V.y, mat.ax, mat.ay);
   float G2 = G1 * SmithG_GGX_Aniso(fabs_(L.z), L.x, L.y, mat.ax, mat.ay);
   float denom = LH + VH * eta;
   denom *= denom;
@@ -393,14 +412,15 @@ RTD f3 EvalSpecRefraction(const Mat& mat, float eta, f3 V, f3 L, f3 H, float& pd
   return sq * (1.0f - mat.metallic) * mat.transmission * (1.0f - F) * D * G2 * fabs_(VH) * jacobian * eta2 /
          fabs_(L.z * V.z);
 }
-RTD f3 EvalClearcoat(const Mat& mat, f3 V, f3 L, f3 H, float& pdf) {  // RT:986-1000 (R23)
+template <bool PRE = false>
+RTD f3 EvalClearcoat(const Mat& mat, f3 V, f3 L, f3 H, float& pdf, const float4* vt = nullptr) {  // RT:986-1000 (R23)
   pdf = 0.0f;
   if (L.z <= 0.0f) return splat(0.0f);
   float VH = dot(V, H);
   float FH = DielectricFresnel(VH, 1.0f / 1.5f);
   float F = mix_(0.04f, 1.0f, FH);
   float D = GTR1(H.z, mat.clearcoatGloss);
-  float G = SmithG_GGX(L.z, 0.25f) * SmithG_GGX(V.z, 0.25f);
+  float G = SmithG_GGX(L.z, 0.25f) * (PRE ? vt[1].z : SmithG_GGX(V.z, 0.25f));
   float jacobian = 1.0f / (4.0f * VH);
   pdf = D * H.z * jacobian;
   return splat(0.25f) * mat.clearcoat * F * D * G / (4.0f * L.z * V.z);
@@ -422,8 +442,28 @@ RTD BsdfFrame bsdf_frame(const Mat& material, f3 V, f3 N) {
   GetSpecColor(material, F.eta, F.specCol, F.sheenCol);
   return F;
 }
+// DisneySample's lobe weights (RT:1083-1084): from the Fresnel term at V.z alone
+RTD void sample_lobe_wts(const BsdfFrame& F, const Mat& material, float& diffuseWt, float& specReflectWt,
+                         float& specRefractWt, float& clearcoatWt) {
+  float approxFresnel = DisneyFresnel(material, F.eta, F.V.z, F.V.z);
+  CalculateBSDFLobePdfs(material, F.specCol, approxFresnel, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
+}
+// the V-only terms of the PRE variants (layout above SampleGGXVNDF), the same operations
+RTD void v_terms(const BsdfFrame& F, const Mat& m, float4* vt) {
+  const f3 V = F.V;
+  float dW, sRW, sTW, cW;
+  sample_lobe_wts(F, m, dW, sRW, sTW, cW);
+  f3 Vh, T1, T2;
+  ggx_vndf_frame(V, m.ax, m.ay, Vh, T1, T2);
+  vt[0] = make_float4(dW, sRW, sTW, cW);
+  vt[1] = make_float4(SchlickFresnel(V.z), SmithG_GGX_Aniso(fabs_(V.z), V.x, V.y, m.ax, m.ay), SmithG_GGX(V.z, 0.25f), Vh.x);
+  vt[2] = make_float4(Vh.y, Vh.z, T1.x, T1.y);
+  vt[3] = make_float4(T1.z, T2.x, T2.y, T2.z);
+}
 
-RTD f3 DisneyEval(const BsdfFrame& F, const Mat& material, f3 N, f3 L, float& bsdfPdf) {  // RT:1002-1067
+template <bool PRE = false>
+RTD f3 DisneyEval(const BsdfFrame& F, const Mat& material, f3 N, f3 L, float& bsdfPdf,
+                  const float4* vt = nullptr) {  // RT:1002-1067
   bsdfPdf = 0.0f;
   f3 f = splat(0.0f);
   const float eta = F.eta;
@@ -439,19 +479,19 @@ RTD f3 DisneyEval(const BsdfFrame& F, const Mat& material, f3 N, f3 L, float& bs
   CalculateBSDFLobePdfs(material, specCol, fresnel, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
   float pdf;
   if (diffuseWt > 0.0f && L.z > 0.0f) {
-    f = f + EvalDiffuse(material, sheenCol, V, L, H, pdf);
+    f = f + EvalDiffuse<PRE>(material, sheenCol, V, L, H, pdf, vt);
     bsdfPdf += pdf * diffuseWt;
   }
   if (specReflectWt > 0.0f && L.z > 0.0f && V.z > 0.0f) {
-    f = f + EvalSpecReflection(material, eta, specCol, V, L, H, pdf);
+    f = f + EvalSpecReflection<PRE>(material, eta, specCol, V, L, H, pdf, vt);
     bsdfPdf += pdf * specReflectWt;
   }
   if (specRefractWt > 0.0f && L.z < 0.0f) {
-    f = f + EvalSpecRefraction(material, eta, V, L, H, pdf);
+    f = f + EvalSpecRefraction<PRE>(material, eta, V, L, H, pdf, vt);
     bsdfPdf += pdf * specRefractWt;
   }
   if (clearcoatWt > 0.0f && L.z > 0.0f && V.z > 0.0f) {
-    f = f + EvalClearcoat(material, V, L, H, pdf);
+    f = f + EvalClearcoat<PRE>(material, V, L, H, pdf, vt);
     bsdfPdf += pdf * clearcoatWt;
   }
   return f * fabs_(L.z);
@@ -460,8 +500,9 @@ RTD f3 DisneyEval(const Mat& material, f3 V, f3 N, f3 L, float& bsdfPdf) {
   return DisneyEval(bsdf_frame(material, V, N), material, N, L, bsdfPdf);
 }
 
+template <bool PRE = false>
 RTD f3 DisneySample(const BsdfFrame& F, float xi_1, float xi_2, float xi_3, const Mat& material, f3 N, f3& L,
-                    float& pdf, bool& isRefract) {  // RT:1070-1161
+                    float& pdf, bool& isRefract, const float4* vt = nullptr) {  // RT:1070-1161
   pdf = 0.0f;
   f3 f = splat(0.0f);
   isRefract = false;
@@ -471,8 +512,12 @@ RTD f3 DisneySample(const BsdfFrame& F, float xi_1, float xi_2, float xi_3, cons
   const f3 T = F.T, B = F.B, V = F.V;
   const f3 specCol = F.specCol, sheenCol = F.sheenCol;
   float diffuseWt, specReflectWt, specRefractWt, clearcoatWt;
-  float approxFresnel = DisneyFresnel(material, eta, V.z, V.z);
-  CalculateBSDFLobePdfs(material, specCol, approxFresnel, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
+  if constexpr (PRE) {
+    const float4 q0 = vt[0];
+    diffuseWt = q0.x; specReflectWt = q0.y; specRefractWt = q0.z; clearcoatWt = q0.w;
+  } else {
+    sample_lobe_wts(F, material, diffuseWt, specReflectWt, specRefractWt, clearcoatWt);
+  }
   float cdf0 = diffuseWt;
   float cdf1 = cdf0 + clearcoatWt;
   L = splat(0.0f);  // R7
@@ -480,29 +525,29 @@ RTD f3 DisneySample(const BsdfFrame& F, float xi_1, float xi_2, float xi_3, cons
     r1 /= cdf0;
     L = CosineSampleHemisphere(r1, r2);
     f3 H = normalize(L + V);
-    f = EvalDiffuse(material, sheenCol, V, L, H, pdf);
+    f = EvalDiffuse<PRE>(material, sheenCol, V, L, H, pdf, vt);
     pdf *= diffuseWt;
   } else if (r1 < cdf1) {
     r1 = (r1 - cdf0) / (cdf1 - cdf0);
     f3 H = SampleGTR1(material.clearcoatGloss, r1);
     if (H.z < 0.0f) H = -H;
     L = normalize(reflect(-V, H));
-    f = EvalClearcoat(material, V, L, H, pdf);
+    f = EvalClearcoat<PRE>(material, V, L, H, pdf, vt);
     pdf *= clearcoatWt;
   } else {
     r1 = (r1 - cdf1) / (1.0f - cdf1);
-    f3 H = SampleGGXVNDF(V, material.ax, material.ay, r1, r2);
+    f3 H = SampleGGXVNDF<PRE>(V, material.ax, material.ay, r1, r2, vt);
     if (H.z < 0.0f) H = -H;
     float fresnel = DisneyFresnel(material, eta, dot(L, H), dot(V, H));  // R7: L == 0 here
     float F = 1.0f - ((1.0f - fresnel) * material.transmission * (1.0f - material.metallic));
     if (xi_3 < F) {
       L = normalize(reflect(-V, H));
-      f = EvalSpecReflection(material, eta, specCol, V, L, H, pdf);
+      f = EvalSpecReflection<PRE>(material, eta, specCol, V, L, H, pdf, vt);
       pdf *= F;
     } else {
       isRefract = true;
       L = normalize(refract(-V, H, eta));  // R14
-      f = EvalSpecRefraction(material, eta, V, L, H, pdf);
+      f = EvalSpecRefraction<PRE>(material, eta, V, L, H, pdf, vt);
       pdf *= (1.0f - F);
     }
     pdf *= specReflectWt + specRefractWt;

@@ -1413,13 +1413,17 @@ RTD HitGeom hit_geom(const KParams& P, int tri, f3 ro, f3 rd) {
 // Camera pass of the bulk groups (RT_CAM_REC): a block-iteration's paths are a few pixels' frames,
 // and every frame of a pixel shades the same camera hit (R6: no jitter).  What depends only on
 // that hit -- geometry, emission, the BSDF frame, or the environment colour of a miss -- is
-// computed once per pixel into LDS (7 float4, kCamRec) by cam_rec and read by the frames' lanes
-// (same functions on the same values: the same bits).  A frame whose own trace result differs
-// from the record's computes everything itself.
+// computed once per pixel into LDS (kCamRec float4) by cam_rec and read by the frames' lanes
+// (same functions on the same values: the same bits), with the terms of the BSDF calls that
+// depend on V and the material alone (v_terms: DisneySample's lobe weights, the VNDF frame, the
+// V-side Fresnel and masking terms; read by the wf_shade<..., CAM> instantiation).  Outside that
+// instantiation a frame whose own trace result differs from the record's computes everything
+// itself; inside it every frame of a pixel has the record's result (the same ray, and a closest
+// hit that is a function of the ray: RT_CHECK reports any frame that does not).
 #ifndef RT_CAM_REC
 #define RT_CAM_REC 1
 #endif
-constexpr int kCamRec = 7;
+constexpr int kCamRec = 11;  // [0..6] the hit, [7..10] v_terms
 RTD void cam_rec(const WFParams& W, const Env& E, unsigned int w, float4* rec) {
   const KParams& P = W.K;
   const WFState& S = W.S;
@@ -1442,6 +1446,7 @@ RTD void cam_rec(const WFParams& W, const Env& E, unsigned int w, float4* rec) {
     rec[4] = make_float4(BF.B.x, BF.B.y, BF.B.z, BF.V.x);
     rec[5] = make_float4(BF.V.y, BF.V.z, BF.specCol.x, BF.specCol.y);
     rec[6] = make_float4(BF.specCol.z, BF.sheenCol.x, BF.sheenCol.y, BF.sheenCol.z);
+    v_terms(BF, m, rec + 7);
   } else {
     const f3 env = P.enable_env ? hdrColor(E, rd) * E.intensity : getDefaultSkyColor(rd.y);
     rec[1] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(r));
@@ -1460,7 +1465,8 @@ RTD BsdfFrame rec_frame(const float4* rec) {
   return F;
 }
 
-template <bool BSDF, bool FUSE = false>  // FUSE: W.fuse_blend is honoured (one-frame pixel groups)
+// CAMK: the camera pass of wf_shade<..., CAM> (every path's hit from its pixel's record)
+template <bool BSDF, bool FUSE = false, bool CAMK = false>  // FUSE: W.fuse_blend is honoured (one-frame pixel groups)
 RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bool camPass, bool loadPrev,
                         unsigned long long& nsamples, const float4* rec = nullptr) {
   const KParams& P = W.K;
@@ -1505,7 +1511,11 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       }
     }
     const int rc0 = S.res[2 * path];
-    useRec = camPass && rec != nullptr && __float_as_int(rec[1].w) == rc0;
+    useRec = CAMK || (camPass && rec != nullptr && __float_as_int(rec[1].w) == rc0);
+#ifdef RT_CHECK
+    if (CAMK && __float_as_int(rec[1].w) != rc0)
+      printf("[rt check] camera record: path %d result %d, record %d\n", path, rc0, __float_as_int(rec[1].w));
+#endif
     float4 oo0, dd0;
     if (camPass) {
       oo0 = make_float4(P.pos[0], P.pos[1], P.pos[2], 0.0f);
@@ -1700,7 +1710,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     if (dot(hN, Ll) > 0.0f) {
       light_fr = light_fr * E.intensity;
       float disney_eval_pdf;
-      const f3 disney_eval_fr = DisneyEval(BF, m, hN, Ll, disney_eval_pdf);
+      const f3 disney_eval_fr = DisneyEval<CAMK>(BF, m, hN, Ll, disney_eval_pdf, CAMK ? rec + 7 : nullptr);
       float mis_weight = misMixWeight(light_pdf, disney_eval_pdf);
       if (!P.enable_mis) mis_weight = 1.0f;
       cnee = mis_weight * hist * light_fr * disney_eval_fr / light_pdf;
@@ -1723,7 +1733,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
     f3 L;
     float pdf;
     bool isRefract;
-    const f3 fr = DisneySample(BF, sx, sy, xi_3, m, hN, L, pdf, isRefract);
+    const f3 fr = DisneySample<CAMK>(BF, sx, sy, xi_3, m, hN, L, pdf, isRefract, CAMK ? rec + 7 : nullptr);
     bool medS = false;
     float scatter_pdf = 0.0f;
     float transmittance = 1.0f;
@@ -1748,7 +1758,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
           L = scatterDir;
         }
       }
-      evf = DisneyEval(BF, m, hN, L, evp);
+      evf = DisneyEval<CAMK>(BF, m, hN, L, evp, CAMK ? rec + 7 : nullptr);
       if (medS && scatter_pdf > 0.0f) {
         evp = scatter_pdf;
         evf = splat(scatter_pdf);
@@ -1805,7 +1815,9 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
 
 // BSDF: enableBSDF (RT:1369 Disney integrator) or the BRDF integrator (RT:1290), one
 // instantiation each so neither carries the other's registers
-template <bool BSDF, bool FUSE = false, int SH_SUB = rtd::SH_SUB>  // SH_SUB: paths per thread and block-iteration
+// CAM: the bulk groups' camera pass (>= 64 frames per group, camera-hit records), its own
+// instantiation: no path state to load, so none of its registers
+template <bool BSDF, bool FUSE = false, int SH_SUB = rtd::SH_SUB, bool CAM = false>  // SH_SUB: paths per thread and block-iteration
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WPE))) void wf_shade(const WFParams W) {
   __shared__ int lq[2 * 256 * SH_SUB];
   __shared__ int la[256 * SH_SUB];
@@ -1818,9 +1830,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
   const unsigned int nfr = (unsigned int)W.n_frames;
-  const bool camrec = RT_CAM_REC && !FUSE && W.cam_n && nfr >= 64u;  // (uniform)
-  const unsigned int na = W.cam_n ? W.cam_n : S.cnt[ca(in)];
-  const unsigned int nq_in = W.cam_n ? W.cam_n : S.cnt[cq(in)];
+  const bool camrec = CAM || (RT_CAM_REC && !FUSE && W.cam_n && nfr >= 64u);  // (uniform)
+  const unsigned int na = CAM || W.cam_n ? W.cam_n : S.cnt[ca(in)];
+  const unsigned int nq_in = CAM || W.cam_n ? W.cam_n : S.cnt[cq(in)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.cnt[kCntFetch] = 0u;  // fetch counter of the next trace pass
     if (na) {
@@ -1849,12 +1861,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __syncthreads();
   // sort only passes holding at least a quarter of the group's path slots (in practice pass 1,
   // whatever the per-rank pixel share)
-  const bool sort_pass = W.pass != 0 && na >= max(1u << 22, (unsigned)W.n_frames * P.n_work / 4u);
+  const bool sort_pass = !CAM && W.pass != 0 && na >= max(1u << 22, (unsigned)W.n_frames * P.n_work / 4u);
   if (!sort_pass) {  // camera pass: hit/miss divergence is low already
 #pragma unroll
     for (int sub = 0; sub < SH_SUB; sub++) {
       const unsigned int j = (unsigned)sub * 256u + threadIdx.x;
-      if (j < nblk) lsort[j] = W.cam_n ? (int)(base + j) : S.active[in][base + j];
+      if (j < nblk) lsort[j] = CAM || W.cam_n ? (int)(base + j) : S.active[in][base + j];
     }
     if (camrec) {  // the block-iteration's pixels' camera hits, one lane each
       const unsigned int p0 = base / nfr, np = (base + nblk - 1u) / nfr - p0 + 1u;
@@ -1888,7 +1900,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
     const float4* rec = camrec ? lrec + kCamRec * ((unsigned)path / nfr - base / nfr) : nullptr;
-    const ShadeOut so = shade_path<BSDF, FUSE>(W, E, path, live, W.cam_n != 0, W.pass != 0, nsamples, rec);
+    const ShadeOut so = shade_path<BSDF, FUSE, CAM>(W, E, path, live, CAM || W.cam_n != 0, !CAM && W.pass != 0, nsamples, rec);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
     // shadow rays from the front of the block's staging list, continuations from the back: the
     // block's queue run is [shadow rays][continuations], so a trace wave's claim is mostly one
