@@ -1826,6 +1826,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __shared__ unsigned int lc[5];  // queue count (shadow rays), active count, queue base, active base, continuations
   constexpr unsigned int kRecs = 256u * SH_SUB / 64u + 1u;  // pixels a block-iteration spans at >= 64 frames
   __shared__ float4 lrec[RT_CAM_REC && !FUSE ? kCamRec * kRecs : 1];
+  // 4 waves/SIMD = 4 blocks per CU: the block's LDS must fit a quarter of the CU's 160 KB
+  static_assert(4 * (2 * 256 * SH_SUB + 2 * 256 * SH_SUB) + 16 * (RT_CAM_REC && !FUSE ? kCamRec * kRecs : 1) +
+                    8 * SH_KEYS + 20 <= 40960,
+                "wf_shade LDS exceeds a quarter of the CU");
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
