@@ -1410,19 +1410,16 @@ RTD HitGeom hit_geom(const KParams& P, int tri, f3 ro, f3 rd) {
   return h;
 }
 
-// Camera pass of the bulk groups (RT_CAM_REC): a block-iteration's paths are a few pixels' frames,
-// and every frame of a pixel shades the same camera hit (R6: no jitter).  What depends only on
-// that hit -- geometry, emission, the BSDF frame, or the environment colour of a miss -- is
-// computed once per pixel into LDS (kCamRec float4) by cam_rec and read by the frames' lanes
-// (same functions on the same values: the same bits), with the terms of the BSDF calls that
-// depend on V and the material alone (v_terms: DisneySample's lobe weights, the VNDF frame, the
-// V-side Fresnel and masking terms; read by the wf_shade<..., CAM> instantiation).  Outside that
-// instantiation a frame whose own trace result differs from the record's computes everything
-// itself; inside it every frame of a pixel has the record's result (the same ray, and a closest
-// hit that is a function of the ray: RT_CHECK reports any frame that does not).
-#ifndef RT_CAM_REC
-#define RT_CAM_REC 1
-#endif
+// Camera pass of the bulk groups (wf_shade<..., CAM>, RT_CAM_SHADE in rt_render.hip): a
+// block-iteration's paths are a few pixels' frames, and every frame of a pixel shades the same
+// camera hit (R6: no jitter).  What depends only on that hit -- geometry, emission, the BSDF frame,
+// or the environment colour of a miss -- is computed once per pixel into LDS (kCamRec float4) by
+// cam_rec and read by the frames' lanes (same functions on the same values: the same bits), with
+// the terms of the BSDF calls that depend on V and the material alone (v_terms: DisneySample's
+// lobe weights, the VNDF frame, the V-side Fresnel and masking terms).  Every frame of a pixel has
+// the record's trace result (the same ray, and a closest hit that is a function of the ray:
+// RT_CHECK reports any frame that does not).  The other instantiations carry none of it (a
+// runtime record path in them cost the later passes' shades 2 ms per 256-frame group).
 constexpr int kCamRec = 11;  // [0..6] the hit, [7..10] v_terms
 RTD void cam_rec(const WFParams& W, const Env& E, unsigned int w, float4* rec) {
   const KParams& P = W.K;
@@ -1482,7 +1479,7 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
   f3 hP = splat(0.0f), hN = splat(0.0f), hV = splat(0.0f);
   float hDist = 0.0f;
   int mat = 0;
-  bool useRec = false;  // camera pass: this path's hit is its pixel's record (cam_rec)
+  constexpr bool useRec = CAMK;  // camera pass of wf_shade<..., CAM>: this path's hit is its pixel's record (cam_rec)
   if (live) {
     float4 cam_d = make_float4(0, 0, 0, 0);
     if (camPass) {  // implicit camera pass: the state a camera path starts with
@@ -1511,7 +1508,6 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       }
     }
     const int rc0 = S.res[2 * path];
-    useRec = CAMK || (camPass && rec != nullptr && __float_as_int(rec[1].w) == rc0);
 #ifdef RT_CHECK
     if (CAMK && __float_as_int(rec[1].w) != rc0)
       printf("[rt check] camera record: path %d result %d, record %d\n", path, rc0, __float_as_int(rec[1].w));
@@ -1825,16 +1821,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __shared__ unsigned int lhist[SH_KEYS], lofs[SH_KEYS];
   __shared__ unsigned int lc[5];  // queue count (shadow rays), active count, queue base, active base, continuations
   constexpr unsigned int kRecs = 256u * SH_SUB / 64u + 1u;  // pixels a block-iteration spans at >= 64 frames
-  __shared__ float4 lrec[RT_CAM_REC && !FUSE ? kCamRec * kRecs : 1];
+  __shared__ float4 lrec[CAM ? kCamRec * kRecs : 1];
   // 4 waves/SIMD = 4 blocks per CU: the block's LDS must fit a quarter of the CU's 160 KB
-  static_assert(4 * (2 * 256 * SH_SUB + 2 * 256 * SH_SUB) + 16 * (RT_CAM_REC && !FUSE ? kCamRec * kRecs : 1) +
+  static_assert(4 * (2 * 256 * SH_SUB + 2 * 256 * SH_SUB) + 16 * (CAM ? kCamRec * kRecs : 1) +
                     8 * SH_KEYS + 20 <= 40960,
                 "wf_shade LDS exceeds a quarter of the CU");
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int in = W.pass & 1, out = in ^ 1;
   const unsigned int nfr = (unsigned int)W.n_frames;
-  const bool camrec = CAM || (RT_CAM_REC && !FUSE && W.cam_n && nfr >= 64u);  // (uniform)
+  constexpr bool camrec = CAM;
   const unsigned int na = CAM || W.cam_n ? W.cam_n : S.cnt[ca(in)];
   const unsigned int nq_in = CAM || W.cam_n ? W.cam_n : S.cnt[cq(in)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -309,14 +309,15 @@ def test_segment_claims_on_tiny_passes(gpu_renderer, env_maps, W, H, n, small):
 @pytest.mark.parametrize("name,W,H,n,small,bsdf,env", [
     ("C3", 24, 16, 256, False, 1, True),   # 128 frames per group: 16 pixels per block-iteration
     ("C3", 20, 13, 130, False, 1, False),  # 65 frames: pixels straddle block-iterations; sky misses
-    ("C4", 16, 11, 200, True, 1, True),    # small-pass kernels (3 paths per thread); glass
+    ("C4", 16, 11, 200, True, 1, True),    # small-pass kernels (no records: every frame computes its hit); glass
     ("C3", 16, 12, 160, False, 0, True),   # BRDF integrator (the record's geometry only)
 ], ids=["C3-128", "C3-65-sky", "C4-small", "C3-brdf"])
 def test_camera_hit_records_match_oracle(gpu_renderer, env_maps, name, W, H, n, small, bsdf, env):
-    """Round 5: with at least 64 frames per group the camera pass's shade computes each pixel's
-    camera hit (geometry, emission, BSDF frame, or the miss colour) once per block-iteration into
-    LDS and the frames read it there (RT_CAM_REC).  Frames of a pixel shade the same hit, so the
-    image and ray count stay the oracle's, bit for bit, in both kernel sets and both integrators."""
+    """Round 5: with at least 64 frames per bulk group the camera pass's shade (wf_shade<..., CAM>)
+    computes each pixel's camera hit (geometry, emission, BSDF frame and the V-only BSDF terms, or
+    the miss colour) once per block-iteration into LDS and the frames read it there.  Frames of a
+    pixel shade the same hit, so the image and ray count stay the oracle's, bit for bit, in both
+    integrators; the small-pass kernels, which keep no records, are checked at the same sizes."""
     from rtamd.renderer import RT_FLAG_NO_FINISH
     sd = cf.config_scene(name)
     fp = cf.frame_params(W, H, flags=RT_FLAG_NO_FINISH if small else 0, enable_env_map=env)
