@@ -1899,6 +1899,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     const unsigned int jj = (unsigned)sub * 256u + threadIdx.x;
     const bool live = jj < nblk;
     int path = live ? lsort[jj] : 0;
+    // (an idle lane's pointer is out of range and never read: shade_path reads rec only for live
+    // paths; clamping it cost the CAM kernel 12 B of scratch)
     const float4* rec = camrec ? lrec + kCamRec * ((unsigned)path / nfr - base / nfr) : nullptr;
     const ShadeOut so = shade_path<BSDF, FUSE, CAM>(W, E, path, live, CAM || W.cam_n != 0, !CAM && W.pass != 0, nsamples, rec);
     const bool qShadow = so.qShadow, qCont = so.qCont, keep = qShadow || qCont;
