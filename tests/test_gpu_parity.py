@@ -311,7 +311,9 @@ def test_segment_claims_on_tiny_passes(gpu_renderer, env_maps, W, H, n, small):
     ("C3", 20, 13, 130, False, 1, False),  # 65 frames: pixels straddle block-iterations; sky misses
     ("C4", 16, 11, 200, True, 1, True),    # small-pass kernels (no records: every frame computes its hit); glass
     ("C3", 16, 12, 160, False, 0, True),   # BRDF integrator (the record's geometry only)
-], ids=["C3-128", "C3-65-sky", "C4-small", "C3-brdf"])
+    ("C4", 16, 11, 192, False, 1, True),   # glass: refraction lobe (G1V) and absorbing medium in the records
+    ("C2", 20, 12, 128, False, 1, True),   # jade: diffuse / fake-subsurface lobe (FV)
+], ids=["C3-128", "C3-65-sky", "C4-small", "C3-brdf", "C4-bulk", "C2-bulk"])
 def test_camera_hit_records_match_oracle(gpu_renderer, env_maps, name, W, H, n, small, bsdf, env):
     """Round 5: with at least 64 frames per bulk group the camera pass's shade (wf_shade<..., CAM>)
     computes each pixel's camera hit (geometry, emission, BSDF frame and the V-only BSDF terms, or
