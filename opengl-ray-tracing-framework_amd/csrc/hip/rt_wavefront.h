@@ -75,7 +75,7 @@ constexpr int kFlagNoRayHist = 1 << 30;  // (internal, development builds) KPara
 
 // WFState::cnt words: the ray-queue counts of the two pass parities (cq), the active-list counts
 // (ca), the trace's / finisher's fetch counter and the claim counters of the 8 queue segments
-// (xcnt, RT_XCD_CLAIMS), one 128-B line each: a device-scope atomic occupies its line ~11 ns (88
+// (xcnt), one 128-B line each: a device-scope atomic occupies its line ~11 ns (88
 // per us per line, whatever the word, and lines scale: tools/atomic_bench.hip,
 // profiles/r05_atomic_throughput.log).  (The pass counters on lines of their own measured
 // neutral, round 5.)
@@ -85,14 +85,11 @@ constexpr unsigned int kCntFetch = 4u;
 __host__ __device__ constexpr unsigned int xcnt(unsigned int s) { return 160u + 32u * s; }
 constexpr unsigned int kCntWords = 160u + 32u * 8u;
 
-// Per-wave statistics flushes of wf_shade / wf_finish (rays, samples, finisher steps): with
-// RT_STATS_SHARDS they go to one of kStatShards 128-B lines after the 128 counters (words 0, 1,
-// 2 of shard s = rays, samples, finish steps), summed by the host, instead of all waves of a
-// launch's end queueing at one line: C3 1080p one-frame calls -6.1% (2.488 -> 2.335 ms
-// synchronised), bulk +0.17% (round 5, profiles/r05_ab_stats_shards_C3.log)
-#ifndef RT_STATS_SHARDS
-#define RT_STATS_SHARDS 1
-#endif
+// Per-wave statistics flushes of wf_shade / wf_finish (rays, samples, finisher steps) go to one of
+// kStatShards 128-B lines after the 128 counters (words 0, 1, 2 of shard s = rays, samples, finish
+// steps), summed by the host, instead of all waves of a launch's end queueing at one line: C3
+// 1080p one-frame calls -6.1% (2.488 -> 2.335 ms synchronised), bulk +0.17% (round 5,
+// profiles/r05_ab_stats_shards_C3.log)
 constexpr unsigned int kStatShards = 64u, kStatWords = 128u + 16u * kStatShards;
 __host__ __device__ constexpr unsigned int stats_shard(unsigned int wave) { return 128u + 16u * (wave % kStatShards); }
 
@@ -357,10 +354,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
 // before finishing the first, and idle lanes refill from the queue.  (Measured and removed: the
 // if-if schedule, while-while and Aila & Laine's speculative while-while)
 
-#ifndef RT_CACHED_LIMIT  // the culling limit kept per ray (1 VGPR) instead of recomputed at every use: C3 bulk
-                         // +0.58% (round 5, profiles/r05_ab_bulk_cached_limit_C3.log; round 2's attempt spilled)
-#define RT_CACHED_LIMIT 1
-#endif
 struct TraceLane {
   // ray as scalars (f3 members made SROA keep the lane in scratch memory)
   float ox, oy, oz, dx, dy, dz, ix, iy, iz;
@@ -368,11 +361,14 @@ struct TraceLane {
   RTD f3 d() const { return mk3(dx, dy, dz); }
   RTD f3 inv() const { return mk3(ix, iy, iz); }
   float best, bestt;
-  float lim;  // RT_CACHED_LIMIT: cull_limit of the current best, updated when best changes
-  RTD float limit(float eps) const { return RT_CACHED_LIMIT ? lim : cull_limit(best, eps, ix, iy, iz); }
+  // cull_limit of the current best, kept per ray (1 VGPR) and updated when best changes instead of
+  // recomputed at every use: C3 bulk +0.58% (round 5, profiles/r05_ab_bulk_cached_limit_C3.log;
+  // round 2's attempt spilled)
+  float lim;
+  RTD float limit(float) const { return lim; }
   RTD void set_best(float d, float eps) {
     best = d;
-    if (RT_CACHED_LIMIT) lim = cull_limit(d, eps, ix, iy, iz);
+    lim = cull_limit(d, eps, ix, iy, iz);
   }
   int besttri, sp, cur, tri_i, tri_end;
   int offNx, offNy, offNz;  // byte offset, inside a QNode, of the near-plane float4 of each axis
@@ -991,7 +987,7 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
   L.dx = __shfl(L.dx, src); L.dy = __shfl(L.dy, src); L.dz = __shfl(L.dz, src);
   L.ix = __shfl(L.ix, src); L.iy = __shfl(L.iy, src); L.iz = __shfl(L.iz, src);
   L.best = __shfl(L.best, src); L.bestt = __shfl(L.bestt, src); L.besttri = __shfl(L.besttri, src);
-  if (RT_CACHED_LIMIT) L.lim = __shfl(L.lim, src);
+  L.lim = __shfl(L.lim, src);
   L.sp = sp_src; L.cur = __shfl(L.cur, src);
   L.tri_i = __shfl(L.tri_i, src); L.tri_end = __shfl(L.tri_end, src);
   L.offNx = __shfl(L.offNx, src); L.offNy = __shfl(L.offNy, src); L.offNz = __shfl(L.offNz, src);
@@ -1020,19 +1016,10 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep static shares + 64-ray claims
 #define RT_GUIDED 2u
 #endif
-#ifndef RT_STATIC_SEG_CLAIMS  // the small passes' dynamic claims from the 8 segments too: C3 1080p one-frame calls
-                              // -1.3% (round 5, profiles/r05_ab_single_segment_claims_C3.log)
-#define RT_STATIC_SEG_CLAIMS 1
-#endif
 #ifndef RT_REFILL_MIN_SMALL  // the small passes' refill threshold: C3 1080p one-frame calls 4 / 6 / 8 / 12 / 16 vs 20:
                              // -0.5 / -0.7 / -1.1, -0.6 / -0.9, -0.5 / -0.7% back-to-back (round 5,
                              // profiles/r05_ab_single_refill_min_small_C3.log; the bulk stays at 20)
 #define RT_REFILL_MIN_SMALL 8
-#endif
-#ifndef RT_XCD_CLAIMS  // bulk passes: 8 queue segments with a claim counter each (below).  C3 bulk -0.13% (noise);
-                       // N=8 rank shares: slowest rank 70.1 / 70.4 -> 69.4 / 69.7 ms (round 5,
-                       // profiles/r05_ab_bulk_segment_claims_C3.log, profiles/r05_rank_sim_segment_claims/)
-#define RT_XCD_CLAIMS 1
 #endif
 #ifndef RT_TAIL_FACTOR  // the tail starts when fewer than grid lanes x this many rays remain
 #define RT_TAIL_FACTOR 4u
@@ -1116,9 +1103,13 @@ void wf_trace(const WFParams W) {
     pool_next = wave_id * static_per;
     pool_end = pool_next + static_per;
   }
-  // RT_XCD_CLAIMS: the bulk pass's queue in 8 segments, each claimed through its own counter
-  // (S.cnt[xcnt(s)], a cache line each); a wave starts on segment blockIdx % 8 (its XCD) and
-  // moves on when a segment is exhausted, drained after 8 empty segments
+  // The pass's queue in 8 segments, each claimed through its own counter (S.cnt[xcnt(s)], a cache
+  // line each); a wave starts on segment blockIdx % 8 (its XCD) and moves on when a segment is
+  // exhausted, drained after 8 empty segments.  Bulk passes: C3 -0.13% (noise), N=8 rank shares
+  // 70.1 / 70.4 -> 69.4 / 69.7 ms (profiles/r05_ab_bulk_segment_claims_C3.log,
+  // profiles/r05_rank_sim_segment_claims/); the small passes after their static shares: C3 1080p
+  // one-frame calls -1.3% (profiles/r05_ab_single_segment_claims_C3.log); round 5, both against
+  // one claim counter for the pass
   unsigned int seg = blockIdx.x & 7u, seg_tries = 0, seg_seen = 0;
   const unsigned int seg_waves = max(1u, part_waves / 8u);
   const int lane = (int)(threadIdx.x & 63);
@@ -1144,14 +1135,14 @@ void wf_trace(const WFParams W) {
     // ---- refill idle lanes from the wave's pool.  A single atomic address sustains only ~90
     // atomics/us, so the pool is claimed in big chunks (P.pool_chunk rays per atomic) while plenty
     // of rays remain and in smaller ones towards the end, so the last rays still spread over all
-    // waves: in the bulk passes from 8 queue segments by guided self-scheduling (RT_XCD_CLAIMS,
-    // RT_GUIDED), in the small passes after their static shares in 64s near the end of the queue.
+    // waves: in the bulk passes from 8 queue segments by guided self-scheduling (RT_GUIDED), in the
+    // small passes from the segments after their static shares, in 64s.
     const unsigned long long idle = __ballot(!busy);
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
     if (idle && !drained && (__popcll(idle) >= (STATIC ? RT_REFILL_MIN_SMALL : RT_REFILL_MIN) || idle == __ballot(true))) {
-      if (RT_XCD_CLAIMS && (!STATIC || RT_STATIC_SEG_CLAIMS) && pool_next >= pool_end) {
+      if (pool_next >= pool_end) {
         while (true) {  // (wave-uniform)
           // (small passes: the segments split what the static shares leave, claimed in 64s)
           const unsigned int d0 = STATIC ? static_total : 0u, dn = nq - d0;
@@ -1175,17 +1166,6 @@ void wf_trace(const WFParams W) {
           }
           seg = (seg + 1u) & 7u;
           seg_seen = 0;
-        }
-      } else if (pool_next >= pool_end) {
-        const unsigned int chunk = (nq - min(pool_end, nq) > tail_rays) ? (unsigned)P.pool_chunk : RT_TAIL_CHUNK;
-        unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&S.cnt[kCntFetch], chunk);
-        base = (STATIC ? static_total : 0u) + __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-        if (base >= nq) {
-          drained = true;
-        } else {
-          pool_next = base;
-          pool_end = min(base + chunk, nq);
         }
       }
       if (!drained || pool_next < pool_end) {
@@ -1840,7 +1820,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
     }
   }
-  if (RT_XCD_CLAIMS && blockIdx.x == 0 && threadIdx.x < 8u) S.cnt[xcnt(threadIdx.x)] = 0u;  // (the same, per segment)
+  if (blockIdx.x == 0 && threadIdx.x < 8u) S.cnt[xcnt(threadIdx.x)] = 0u;  // (the next trace pass's segment counters)
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1931,8 +1911,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     nsamples += __shfl_xor(nsamples, off);
   }
   if ((threadIdx.x & 63) == 0 && (nrays | nsamples)) {
-    // (RT_STATS_SHARDS: the launch's last waves all flush at once; spread over shard lines)
-    unsigned long long* st = RT_STATS_SHARDS ? P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6)) : P.stats;
+    // (the launch's last waves all flush at once: spread over the shard lines)
+    unsigned long long* st = P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6));
     atomicAdd(&st[0], nrays);
     atomicAdd(&st[1], nsamples);
   }
@@ -2148,10 +2128,10 @@ void wf_finish(const WFParams W) {
     nsteps += __shfl_xor(nsteps, off);
   }
   if (lane == 0) {
-    unsigned long long* st = RT_STATS_SHARDS ? P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6)) : P.stats;
+    unsigned long long* st = P.stats + stats_shard(blockIdx.x * 4u + (threadIdx.x >> 6));
     atomicAdd(&st[0], nrays);
     atomicAdd(&st[1], nsamples);
-    atomicAdd(&st[RT_STATS_SHARDS ? 2 : 20], nsteps);  // rt_stats.finish_steps
+    atomicAdd(&st[2], nsteps);  // rt_stats.finish_steps
   }
 }
 
