@@ -1792,18 +1792,18 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
 #endif
           // (bulk groups: RT_SH_SUB_BULK paths per thread and block-iteration)
           const bool bulk_shade = slots_g[g] > c->finish_slots && !WP.fuse_blend;
-          const unsigned int sub = bulk_shade ? (unsigned)rtd::SH_SUB_BULK : (unsigned)rtd::SH_SUB;
           // (the camera pass of a bulk group with >= 64 frames: camera-hit records, wf_shade<..., CAM>)
           const bool cam_shade = RT_CAM_SHADE && bulk_shade && WP.cam_n && WP.n_frames >= 64;
+          const unsigned int sub = cam_shade ? (unsigned)rtd::SH_SUB_CAM : bulk_shade ? (unsigned)rtd::SH_SUB_BULK : (unsigned)rtd::SH_SUB;
           const unsigned int shade_grid = std::max(1u, std::min<unsigned int>(4096u, (slots_g[g] + 256u * sub - 1) / (256u * sub)));
           if (fp->enable_bsdf) {
             if (WP.fuse_blend) hipLaunchKernelGGL((rtd::wf_shade<true, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
-            else if (cam_shade) hipLaunchKernelGGL((rtd::wf_shade<true, false, rtd::SH_SUB_BULK, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+            else if (cam_shade) hipLaunchKernelGGL((rtd::wf_shade<true, false, rtd::SH_SUB_CAM, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
             else if (bulk_shade) hipLaunchKernelGGL((rtd::wf_shade<true, false, rtd::SH_SUB_BULK>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
             else hipLaunchKernelGGL((rtd::wf_shade<true, false>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
           } else {
             if (WP.fuse_blend) hipLaunchKernelGGL((rtd::wf_shade<false, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
-            else if (cam_shade) hipLaunchKernelGGL((rtd::wf_shade<false, false, rtd::SH_SUB_BULK, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
+            else if (cam_shade) hipLaunchKernelGGL((rtd::wf_shade<false, false, rtd::SH_SUB_CAM, true>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
             else if (bulk_shade) hipLaunchKernelGGL((rtd::wf_shade<false, false, rtd::SH_SUB_BULK>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
             else hipLaunchKernelGGL((rtd::wf_shade<false, false>), dim3(shade_grid), dim3(256), 0, sg[g], WP);
           }

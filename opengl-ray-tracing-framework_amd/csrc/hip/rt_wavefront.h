@@ -1352,7 +1352,11 @@ RTD int shade_key(const KParams& P, const WFState& S, int path) {
 #ifndef RT_SHADE_WPE  // 4 waves/SIMD (<= 128 VGPRs, 12 B/lane spill): shade -8% vs the natural 3
 #define RT_SHADE_WPE 4
 #endif
-constexpr int SH_SUB = RT_SH_SUB, SH_SUB_BULK = RT_SH_SUB_BULK;
+#ifndef RT_SH_SUB_CAM  // the bulk camera pass's shade (wf_shade<..., CAM>): 6 / 4 vs 8 -0.22 / -0.53% (C3 bulk,
+                       // round 5, profiles/r05_ab_bulk_cam_shade_sub_C3.log)
+#define RT_SH_SUB_CAM RT_SH_SUB_BULK
+#endif
+constexpr int SH_SUB = RT_SH_SUB, SH_SUB_BULK = RT_SH_SUB_BULK, SH_SUB_CAM = RT_SH_SUB_CAM;
 
 // One path's shade step (the body of wf_shade, shared with wf_finish): consume the traced results
 // of the current bounce, sample the next one, write the state back and return the rays to queue.
