@@ -48,6 +48,7 @@ struct KParams {
   int qroot;
   int n_qnodes, n_tri;              // (bounds of the RT_CHECK development build)
   int lds_entries;                  // wavefront traversal: stack entries kept in LDS
+  int stack_cap;                    // the deepest stack of the scene's trees (a lane-quad move copies up to it)
   float cull_eps;                   // culling bound: accepted hit points lie within this of their box
   int pool_chunk;                   // wavefront traversal: rays claimed per queue atomic
   int2* __restrict__ stack_ovf;     // deeper entries: [entry - lds_entries][grid lane]

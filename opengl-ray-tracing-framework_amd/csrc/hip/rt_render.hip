@@ -651,8 +651,8 @@ int occupancy(rt_ctx* c) {
 // (DESIGN.md §4, round 5): entry j in [KL, entries) of grid lane l of path-state set `set` lives at
 // element set * ovf_group + (j - KL) * ovf_lanes + l, with ovf_lanes = trace grid blocks * 256 and
 // l below that (the finisher's grid is never larger than the trace grid); a lane-quad move copies
-// at most KL + 64 entries.  entries = the deepest stack of the scene's trees (3 * qdepth + 2 for
-// the 4-wide one).
+// at most `entries` = the deepest stack of the scene's trees (3 * qdepth + 2 for the 4-wide one),
+// passed to the kernels as KParams::stack_cap.
 std::string ovf_layout_error(const rt_ctx* c, int set, unsigned int trace_grid_blocks) {
   const int entries = std::max(c->stack_entries, c->qstack_entries);
   const int kl = c->trace_lds_entries;
@@ -671,10 +671,6 @@ std::string ovf_layout_error(const rt_ctx* c, int set, unsigned int trace_grid_b
   if ((unsigned)(c->finish_bpc * c->n_cus) > trace_grid_blocks || c->pipe_finish_bpc > c->finish_bpc) {
     snprintf(buf, sizeof buf, "overflow stack: finisher grid %d x %d above the trace grid %u", c->finish_bpc,
              c->n_cus, trace_grid_blocks);
-    return buf;
-  }
-  if (entries > kl + 64) {
-    snprintf(buf, sizeof buf, "overflow stack: %d entries, a lane-quad move copies %d", entries, kl + 64);
     return buf;
   }
   return std::string();
@@ -1493,6 +1489,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
     P.cost_blocks = c->cost_blocks ? 1 : 0;
     P.n_work = (unsigned)c->local_tiles * (unsigned)(c->tile_w * c->tile_h);
     P.nodes = c->d_nodes; P.root = c->root; P.has_scene = c->has_scene; P.stack_entries = c->stack_entries;
+    P.stack_cap = std::max(c->stack_entries, c->qstack_entries);
     P.qnodes = c->d_qnodes; P.qroot = c->qroot; P.n_qnodes = c->n_qnodes; P.n_tri = c->n_tri;
     {  // eps of the culling bound for this call's origins (camera position, scene points)
       double R = c->cull_R;

@@ -391,6 +391,9 @@ struct TraceStack {
   gu64* ovf;      // the block's overflow columns: entry j >= KL of block lane l at ovf[(j - KL) * ovs + l]
   unsigned ovs;
   int KL;
+#ifdef RT_CHECK
+  int cap;  // KParams::stack_cap: the overflow columns hold entries KL .. cap - 1
+#endif
   RTD uint32_t lane() const {
     uint32_t l = (lds_addr(lds) - lds_addr(lds0)) >> 3;
     asm volatile("" : "+v"(l));  // recomputed where used: a hoisted 64-bit address would live in scratch
@@ -400,7 +403,7 @@ struct TraceStack {
   // across the traversal loop)
   RTD gu64* ovf_at(int j) const {
 #ifdef RT_CHECK
-    if (j < KL || j >= KL + 64) printf("[rt check] overflow stack index %d (KL %d)\n", j, KL);
+    if (j < KL || j >= cap) printf("[rt check] overflow stack index %d (KL %d, cap %d)\n", j, KL, cap);
 #endif
     return ovf + (size_t)(j - KL) * ovs + lane();
   }
@@ -962,9 +965,10 @@ RTD bool tl_coop_step(const KParams& P, TraceLane& L, const TraceStack& TS, bool
 // G*g .. G*g+G-1 take the traversal state of the g-th live lane (registers by lane permutes; the LDS stack column and
 // its overflow entries entry by entry, every lane reading entry j of its source before any lane
 // writes entry j of its own).  Returns this lane's source (itself when its group holds no ray).
-// Every lane of the wave must be active.
+// Every lane of the wave must be active.  cap = the deepest stack of the scene's trees (KParams::
+// stack_cap), which the overflow columns are sized for: a deeper scene moves its whole stacks.
 template <int G>
-RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, int lane) {
+RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, int lane, int cap) {
   const int nl = __popcll(live);
   const int g = lane / G;
   unsigned long long m = live;
@@ -972,7 +976,7 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
   const int src = (g < nl && m) ? (int)__builtin_ctzll(m) : lane;
   // (only the sources count: a lane that holds no ray may have no defined stack)
   const int sp_src = __shfl(L.sp, src);
-  int spm = g < nl ? min(max(sp_src, 0), TS.KL + 64) : 0;
+  int spm = g < nl ? min(max(sp_src, 0), cap) : 0;
   for (int o = 32; o > 0; o >>= 1) spm = max(spm, __shfl_xor(spm, o));
   const uint32_t w0 = threadIdx.x & ~63u;
   for (int j = 0; j < min(spm, TS.KL); j++) {
@@ -1075,6 +1079,9 @@ void wf_trace(const WFParams W) {
   // overflow region ([entry][grid lane], coalesced) that only very deep stacks touch.
   TraceStack TS;
   TS.KL = P.lds_entries;
+#ifdef RT_CHECK
+  TS.cap = P.stack_cap;
+#endif
   TS.lds0 = reinterpret_cast<int2*>(smem);
   TS.lds = TS.lds0 + threadIdx.x;
   TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
@@ -1165,7 +1172,9 @@ void wf_trace(const WFParams W) {
             break;
           }
           seg = (seg + 1u) & 7u;
-          seg_seen = 0;
+          // unknown fill of the next segment (it may be nearly drained): its first claim is the
+          // tail chunk, later ones are guided by the counter value that claim returned
+          seg_seen = 0xFFFFFFFFu;
         }
       }
       if (!drained || pool_next < pool_end) {
@@ -1210,7 +1219,7 @@ void wf_trace(const WFParams W) {
       const int nl = __popcll(live);
       if (nl > 0 && nl <= RT_TRACE_COOP) {
         coop = true;
-        const int src = coop_move<4>(L, TS, live, lane);
+        const int src = coop_move<4>(L, TS, live, lane, P.stack_cap);
         const int e_src = __shfl(entry, src), b_src = __shfl((int)busy, src);
         entry = e_src;
         busy = (lane >> 2) < nl && b_src != 0;
@@ -1531,7 +1540,10 @@ RTD ShadeOut shade_path(const WFParams& W, const Env& E, int path, bool live, bo
       fin = Le0 + Lo;
       doFinish = true;
     } else {
-      const int r = rc0;
+      // the CAM pass branches on the record's own result (rec[1].w, written on hit and miss alike),
+      // so both record branches read initialised LDS; a frame whose own result differed would be
+      // reported by the RT_CHECK build above (none is: every frame traces the same camera ray, R6)
+      const int r = useRec ? __float_as_int(rec[1].w) : rc0;
       const float4 oo = oo0, dd = dd0;
       const f3 ro = xyz(oo), rd = xyz(dd);
       if (useRec && r >= 0) {  // the pixel's camera hit from the record (cam_rec)
@@ -1972,6 +1984,9 @@ void wf_finish(const WFParams W) {
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
   TraceStack TS;
   TS.KL = P.lds_entries;
+#ifdef RT_CHECK
+  TS.cap = P.stack_cap;
+#endif
   TS.lds0 = reinterpret_cast<int2*>(smem);
   TS.lds = TS.lds0 + threadIdx.x;
   TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
@@ -2044,7 +2059,7 @@ void wf_finish(const WFParams W) {
       const int nl = __popcll(live);
       if (nl > 0 && nl <= RT_FINISH_COOP) {
         // the g-th path moves to lanes 4g .. 4g+3
-        const int src = coop_move<4>(L, TS, live, lane);
+        const int src = coop_move<4>(L, TS, live, lane, P.stack_cap);
         const int g = lane / 4;
         coop = 4;
         path = __shfl(path, src);

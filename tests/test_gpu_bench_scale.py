@@ -1,0 +1,170 @@
+"""bench.py's exact operating point at full scale, pinned bit for bit against the oracle (VERDICT r5
+item 1).
+
+The other full-size tests render 1-2 frames of 1080p: <= 4.1 M path slots per frame group, below
+the finisher's 8 Mi limit, so they run the small-pass (`STATIC`) kernels and `wf_finish`.  The
+bench runs something else: 1024-frame steps at loopNum ~1 .. 25,600 whose frame groups of 256
+(N = 1) or 512 (a rank share of N = 8) frames are hundreds of millions of slots, traced by the bulk
+`wf_trace` (guided 1,024-ray claims from 8 queue segments, overflow stacks over the whole grid),
+shaded by `wf_shade<..., CAM>` (LDS camera records) and blended by `wf_blend`.  Here that exact
+shape renders C3 at 1920x1080 and the oracle re-renders scattered 8x8 windows of it (the sky, the
+floor, the loong's silhouette and coils: the costliest tiles by rt_tile_costs) from the same
+host-written history; every pixel of every window must equal the GPU's bits.
+
+* N = 1: the bench's path-state budget (1024 frames x the rank's 32-px tiles), loopNum 24,001 ..
+  25,024 (the last warm-up/timed steps' Sobol indices and randOrigins), which the library runs as
+  two launches of 512 frames, two frame groups of 256 each.
+* N = 8, rank 0 of the cost-balanced map of 16-px tiles (bench.py's per-rank share of the SCALE
+  run): one 1,024-frame launch of two 512-frame groups.
+
+Reference: fragment_shader_ray_tracing.glsl:1518-1558 (main: seed, camera ray, path, blend),
+main.cpp:175-200 (one frame per loop pass, loopNum += 1).
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from helpers import bit_mismatch, frames_for
+from rtamd import configs as cf
+from rtamd import tiling
+
+pytestmark = pytest.mark.gpu
+
+W, H = 1920, 1080
+FIRST, N_FRAMES = 24001, 1024
+WIN = 8
+
+
+def _oracle_windows(sd, env, frames, hist, windows):
+    """Oracle accumulation of every (x0, y0) WIN x WIN window, one host thread per window."""
+    import oracle as orc
+    scene = orc.OracleScene(sd.tri_enc, sd.node_enc, env[0], env[1])
+
+    def one(xy):
+        x0, y0 = xy
+        acc, cnt = orc.render(scene, frames, W, H, x0=x0, y0=y0, w=WIN, h=WIN,
+                              accum=hist[y0:y0 + WIN, x0:x0 + WIN], threads=1)
+        return acc, cnt["rays"]
+
+    with ThreadPoolExecutor(max_workers=16) as ex:
+        return list(ex.map(one, windows))
+
+
+def _windows(costs, tiles, tile, n_costly, n_spread, seed):
+    """n_costly windows in the costliest of `tiles` (the loong: silhouette and coils) and n_spread
+    at seeded places in the rest (sky, floor); each inside its tile, at a seeded offset."""
+    rng = np.random.default_rng(seed)
+    tiles = np.asarray(tiles)
+    by_cost = tiles[np.argsort(-np.asarray(costs)[tiles], kind="stable")]
+    pick = list(by_cost[:n_costly]) + list(rng.choice(by_cost[n_costly:], n_spread, replace=False))
+    out = []
+    for t in pick:
+        x0, y0, w, h = tiling.tile_rect(int(t), W, H, tile, tile)
+        if w < WIN or h < WIN:
+            continue
+        out.append((x0 + int(rng.integers(0, w - WIN + 1)), y0 + int(rng.integers(0, h - WIN + 1))))
+    return out
+
+
+def _render_bench_shape(sd, env, fp, ro, hist, tile, rank, world, owner):
+    from rtamd.renderer import Renderer
+    r = Renderer(0)
+    try:
+        r.set_scene_soa(sd.soa, sd.nodes)
+        r.set_env(*env)
+        r.resize(W, H, tile=tile, rank=rank, world=world)
+        if owner is not None:
+            r.set_tile_owners(owner)
+        ad = r.accum_device()
+        r.set_max_paths(N_FRAMES * ad["local_tiles"] * tile * tile)  # bench.py main()
+        r.write_accum(hist)
+        r.set_loop_num(FIRST - 1)
+        r.reset_stats()
+        st = r.render(fp, ro)
+        assert r.loop_num == FIRST + N_FRAMES - 1
+        return r.read_accum(), st, ad["local_tiles"]
+    finally:
+        r.close()
+
+
+def _tile_costs(sd, env, fp, ro, tile):
+    from rtamd.renderer import Renderer
+    r = Renderer(0)
+    try:
+        r.set_scene_soa(sd.soa, sd.nodes)
+        r.set_env(*env)
+        r.resize(W, H, tile=tile)
+        return r.tile_costs(fp, ro[-1:])
+    finally:
+        r.close()
+
+
+@pytest.fixture(scope="module")
+def bench_inputs(env_maps):
+    sd = cf.config_scene("C3")
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, FIRST, N_FRAMES, ro_offset=FIRST - 1)
+    hist = np.random.default_rng(7).uniform(0.0, 2.0, (H, W, 3)).astype(np.float32)
+    return sd, fp, ro, frames, hist
+
+
+def _check(img, sd, env, frames, hist, windows, owned=None):
+    assert len(windows) >= 12
+    ref = _oracle_windows(sd, env, frames, hist, windows)
+    bad = []
+    for (x0, y0), (acc, rays) in zip(windows, ref):
+        assert rays > 0
+        got = img[y0:y0 + WIN, x0:x0 + WIN]
+        frac, diff = bit_mismatch(got, acc)
+        if frac:
+            bad.append(((x0, y0), int(diff.sum())))
+        # the windows were accumulated from a history of up to 2.0: a pixel equal to it would
+        # mean the render never reached it
+        assert not np.array_equal(got, hist[y0:y0 + WIN, x0:x0 + WIN])
+    assert not bad, f"windows differing from the oracle (origin, pixels): {bad}"
+
+
+def test_bench_step_full_scale_matches_oracle_windows(env_maps, bench_inputs):
+    sd, fp, ro, frames, hist = bench_inputs
+    tile = 32  # bench.py --tile default at N = 1
+    img, st, n_local = _render_bench_shape(sd, env_maps, fp, ro, hist, tile, 0, 1, None)
+    # the bench's shape: two 512-frame launches (206 GB of path state each), 2 frame groups of
+    # 256 frames x 9 passes, all on the bulk kernels (no finisher), every pixel-frame sampled
+    assert st["launches"] == 2, st
+    assert st["trace_launches"] == 2 * 2 * 9, st
+    assert st["finish_steps"] == 0
+    assert st["samples"] == W * H * N_FRAMES
+    rays_per_sample = st["rays"] / st["samples"]
+    assert 2.2 < rays_per_sample < 2.5, rays_per_sample  # bench line: 2.347
+    costs = _tile_costs(sd, env_maps, fp, ro, tile)
+    n_tiles = len(tiling.modulo_owners(W, H, tile, tile, 1))
+    assert n_local == n_tiles == len(costs)
+    windows = _windows(costs, range(n_tiles), tile, 10, 6, seed=11)
+    # plus two windows straddling tile corners (pixels of four tiles)
+    windows += [(tile * 29 - 4, tile * 17 - 4), (tile * 41 - 4, tile * 9 - 4)]
+    _check(img, sd, env_maps, frames, hist, windows)
+
+
+def test_bench_rank_share_n8_matches_oracle_windows(env_maps, bench_inputs):
+    sd, fp, ro, frames, hist = bench_inputs
+    tile, world, rank = 16, 8, 0  # bench.py at N > 1: 16-px tiles, cost-balanced owner map
+    costs = _tile_costs(sd, env_maps, fp, ro, tile)
+    owner = tiling.balance(costs, world)
+    img, st, n_local = _render_bench_shape(sd, env_maps, fp, ro, hist, tile, rank, world, owner)
+    mine = tiling.local_tiles(W, H, tile, tile, rank, world, owner)
+    assert n_local == len(mine)
+    # one launch holds the whole 1024-frame step (51 GB of path state): two groups of 512
+    assert st["launches"] == 1, st
+    assert st["trace_launches"] == 2 * 9, st
+    assert st["finish_steps"] == 0
+    npx = sum(tiling.tile_rect(t, W, H, tile, tile)[2] * tiling.tile_rect(t, W, H, tile, tile)[3] for t in mine)
+    assert st["samples"] == npx * N_FRAMES
+    # pixels of other ranks' tiles stay as the history left them (not rendered here): read back as 0
+    others = np.ones((H, W), bool)
+    for t in mine:
+        x0, y0, w, h = tiling.tile_rect(t, W, H, tile, tile)
+        others[y0:y0 + h, x0:x0 + w] = False
+    assert not img[others].any()
+    windows = _windows(costs, mine, tile, 10, 6, seed=13)
+    _check(img, sd, env_maps, frames, hist, windows)

@@ -6,6 +6,8 @@ BASELINE.json's north star ("within a stated fp32 tolerance") is here 0 ulp.  Th
 admitted deviation is the closest-hit culling of the GPU traversal, which changes nothing
 but exact-tie order; the culled and exhaustive GPU paths are both checked.
 """
+from types import SimpleNamespace
+
 import numpy as np
 import pytest
 
@@ -211,6 +213,79 @@ def test_lane_quads_move_overflow_stacks(gpu_dev_renderer, env_maps, monkeypatch
     ref, cnt = oracle_render(sd, env_maps, W, H, frames)
     monkeypatch.setenv("RT_LDS_STACK", "1")
     img, st = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
+    assert st["rays"] == cnt["rays"], (st, cnt)
+    assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def _deep_chain_scene(depth=64):
+    """A BVH at the library's depth limit (rt_set_scene: RT_ERR_LIMIT beyond 64 levels): `depth`
+    stacked triangles in planes z = const facing the camera, in a chain tree whose level i has the
+    farthest remaining triangle as one child and the rest as the other, so a ray through the stack
+    enters the near chain first and pushes a far child on every level (Triangle_encoded /
+    BVHNode_encoded, src/core/Triangle.h:28-39, src/core/BVH.h:17-21)."""
+    n = depth
+    mats = [cf.MATERIALS["brown_glass"].texels(), cf.MATERIALS["jade"].texels()]
+    tri = np.zeros((n, 14, 3), np.float32)
+    box = []
+    for t in range(n):  # t = 0 farthest (z = -3.15) ... n - 1 nearest (z = 0)
+        z = np.float32(-0.05 * (n - 1 - t))
+        dx, dy = 0.03 * np.sin(t), 0.03 * np.cos(t)
+        p = np.array([(-7.5 + dx, -4.2 + dy, z), (7.6 + dx, -4.0 + dy, z), (0.1 + dx, 5.5 + dy, z)], np.float32)
+        tri[t, 0:3] = p
+        tri[t, 3:6] = (0.0, 0.0, 1.0)
+        tri[t, 6:14] = mats[t % 2].reshape(8, 3)
+        box.append((p.min(0), p.max(0)))
+    nodes = np.zeros((2 * n, 4, 3), np.float32)
+
+    def leaf(j, t):
+        nodes[j, 1] = (1, t, 0)
+        nodes[j, 2], nodes[j, 3] = box[t]
+
+    # internal level i (1-based, root = node 1) is node 2i-1: left = the far leaf 2i holding
+    # triangle i-1, right = the chain 2i+1 (on the last level the leaf of the nearest triangle)
+    for i in range(n - 1, 0, -1):
+        j, lj, rj = 2 * i - 1, 2 * i, 2 * i + 1
+        leaf(lj, i - 1)
+        if i == n - 1:
+            leaf(rj, n - 1)
+        lo = np.min([b[0] for b in box[i - 1:]], 0)
+        hi = np.max([b[1] for b in box[i - 1:]], 0)
+        nodes[j, 0] = (lj, rj, 0)
+        nodes[j, 2], nodes[j, 3] = lo, hi
+    return tri, nodes
+
+
+def test_bvh_deeper_than_the_limit_is_refused(gpu_renderer):
+    """65 levels: rt_set_scene fails with RT_ERR_LIMIT (rt_abi.h), it does not render wrongly."""
+    tri, nodes = _deep_chain_scene(65)
+    with pytest.raises(RuntimeError) as e:
+        gpu_renderer.set_scene_encoded(tri, nodes)
+    assert "deeper than 64" in str(e.value)
+
+
+@pytest.mark.parametrize("dev", [False, True])
+def test_deepest_bvh_renders_and_moves_whole_stacks(gpu_renderer, gpu_dev_renderer, env_maps, monkeypatch, dev):
+    """A chain BVH at the depth limit renders bit-exact, including its lane-quad moves:
+    the moves copy a path's whole stack, up to the scene's deepest (KParams::stack_cap), where they
+    used to stop at LDS + 64 entries and the host refused any scene deeper than that.  The dev
+    variant keeps the reference's own chain as the 4-wide tree (RT_REBUILD=0: 3 pushes per 4-wide
+    node, ~64 stacked entries) with one LDS entry per lane (RT_LDS_STACK=1), so nearly the whole
+    stack sits in the overflow columns when the small passes' tails and the finisher move it."""
+    from rtamd.renderer import RT_FLAG_FINISH
+    tri, nodes = _deep_chain_scene(64)
+    W, H = 80, 48
+    cam = sl.camera(-90.0, 0.0, cf.CAMERA_ZOOM, float(np.float32(W) / np.float32(H)))
+    fp = cf.frame_params(W, H, flags=RT_FLAG_FINISH, front=cam["front"], right=cam["right"], up=cam["up"],
+                         left_bottom_corner=cam["left_bottom_corner"], half_h=cam["half_h"], half_w=cam["half_w"])
+    ro, frames = frames_for(fp, 1, 2)
+    import oracle as orc
+    ref, cnt = orc.render(orc.OracleScene(tri, nodes, env_maps[0], env_maps[1]), frames, W, H)
+    r = gpu_renderer
+    if dev:
+        monkeypatch.setenv("RT_LDS_STACK", "1")
+        monkeypatch.setenv("RT_REBUILD", "0")
+        r = gpu_dev_renderer
+    img, st = gpu_render(r, SimpleNamespace(tri_enc=tri, node_enc=nodes), env_maps, W, H, fp, ro, encoded=True)
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert bit_mismatch(img, ref)[0] == 0.0
 
