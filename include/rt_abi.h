@@ -42,7 +42,10 @@
  *    steps, which it included before, are finish_steps (their sum is the old path_steps).
  * 5: rt_stats_get and rt_render write the ABI-3 struct only (the 104 bytes through p1_rays, what
  *    every binding of an ABI-3 header allocated; ABI 4 wrote past them), and the fields added in 4
- *    reach a caller only through rt_stats_get_sized with its own sizeof(rt_stats).
+ *    reach a caller only through rt_stats_get_sized with its own sizeof(rt_stats).  A binding
+ *    written against the ABI-4 header (whose rt_stats_get filled the whole struct) must switch to
+ *    rt_stats_get_sized(ctx, &s, sizeof s) to keep pass0_steps .. trace_busy_ms: the layout is
+ *    unchanged, so that call with the ABI-4 size fills them (tests/c/abi_stats.c).
  *    RT_FLAG_SORTED_TRAVERSAL is accepted and has no effect (the octant-ordered traversal it
  *    switched off was removed).
  * A binding checks rt_abi_version() at load time. */

@@ -82,3 +82,28 @@ def test_flag_constants_match_header():
     binding = {k: getattr(renderer, k) for k in dir(renderer) if k.startswith("RT_FLAG_")}
     assert len(header) >= 7
     assert header == binding
+
+
+C_BIN = ROOT / "tests" / "c" / "bin" / "abi_stats"
+
+
+def test_c_binding_builds_against_the_header():
+    """tests/c/abi_stats.c (built by __graft_entry__.build() with gcc) links librtamd.so the way a
+    C caller of include/rt_abi.h does; without a GPU it must fail cleanly in rt_create."""
+    import subprocess
+    import torch
+    assert C_BIN.exists(), "make -C tests/c"
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: tests/test_abi.py::test_c_binding_reads_the_abi4_tail runs it")
+    p = subprocess.run([str(C_BIN)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "rt_create" in p.stderr, (p.returncode, p.stderr)
+
+
+@pytest.mark.gpu
+def test_c_binding_reads_the_abi4_tail():
+    """a C caller compiled against this header gets the ABI-4 fields of rt_stats through
+    rt_stats_get_sized, and rt_stats_get writes only the ABI-3 prefix (tests/c/abi_stats.c)."""
+    import subprocess
+    p = subprocess.run([str(C_BIN)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert "abi_stats ok" in p.stdout
