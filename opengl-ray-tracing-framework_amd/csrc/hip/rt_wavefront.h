@@ -2255,11 +2255,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
 // bound to stay there (2 waves: coop +3.6% instead of -6.6%)
 #define RT_FINISH_WPE 3
 #endif
-#ifndef RT_FINISH_HAND  // intra-block hand-off (0: off): a drained wave other than its block's first with at
-// most this many paths left hands each path, at its next shade boundary, to the block's first wave
-// (the collector) through an LDS list, and exits when empty (round 6)
-#define RT_FINISH_HAND 0
-#endif
 template <bool BSDF, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_FINISH_WPE)))
 void wf_finish(const WFParams W) {
@@ -2269,28 +2264,6 @@ void wf_finish(const WFParams W) {
   const int in = W.pass & 1;
   const unsigned int na = S.cnt[ca(in)];
   const int lane = (int)(threadIdx.x & 63);
-  // Hand-off (RT_FINISH_HAND).  A path between bounces lives in its path-state rows (shade_path
-  // wrote them, rays included), so passing it on is passing its index.  Only within the block:
-  // its waves share the CU's L1 and LDS, so the rows a producer wrote (waited for before the
-  // index is published) are what the collector reads, and no wave ever waits for a wave that is
-  // not resident.  fh_out counts the paths the block holds (in lanes or in the list): +1 per
-  // claim from the active list, -1 per path end; the collector exits only when it is 0, so
-  // every handed-off path is taken.  The list is a ring of 256: the block holds at most 256
-  // paths (one per lane; a hand-off frees its lane and drained waves claim nothing).
-  __shared__ int fh_q[RT_FINISH_HAND ? 256 : 1];
-  __shared__ unsigned int fh_tail;
-  __shared__ int fh_out;
-  if (RT_FINISH_HAND) {
-    fh_q[threadIdx.x] = -1;
-    if (threadIdx.x == 0) {
-      fh_tail = 0u;
-      fh_out = 0;
-    }
-    __syncthreads();
-  }
-  const bool collector = RT_FINISH_HAND && (threadIdx.x >> 6) == 0;
-  unsigned int fh_head = 0u;  // (collector) the next list entry to take
-  bool handing = false;       // (other waves) paths go to the collector at their shade boundaries
   // only as many waves as the list can feed take part (one lane per path)
   if ((blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6)) * 64u >= na) return;
   TraceStack TS;
@@ -2344,9 +2317,7 @@ void wf_finish(const WFParams W) {
     tl_start<WIDE>(P, L);
   };
   while (true) {
-    // idle lanes take the next paths of the active list (one atomic per wave), then (the
-    // collector) handed-off ones; one begin_rays site for both
-    int np = -1;
+    // idle lanes take the next paths of the active list (one atomic per wave)
     const unsigned long long idle = __ballot(st == FS_IDLE);
     if (idle && !drained) {
       const unsigned int want = (unsigned int)__popcll(idle);
@@ -2357,47 +2328,20 @@ void wf_finish(const WFParams W) {
 #ifdef RT_FINISH_PROF
       if (base < na) prof_paths += min(want, na - base);
 #endif
-      if (st == FS_IDLE && idx < na) np = S.active[in][idx];
-      if (RT_FINISH_HAND && lane == 0 && base < na) atomicAdd(&fh_out, (int)min(want, na - base));
+      if (st == FS_IDLE && idx < na) {
+        path = S.active[in][idx];
+        const uint32_t flags = S.s5[path].y & 0xffu;
+        st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
+        begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
+      }
       drained = base + want >= na;
     }
-    if (RT_FINISH_HAND && collector && coop == 0) {  // idle lanes take handed-off paths
-      const unsigned long long fidle = __ballot(st == FS_IDLE && np < 0);
-      const unsigned int avail = *(volatile unsigned int*)&fh_tail - fh_head;
-      const unsigned int k = min((unsigned int)__popcll(fidle), avail);
-      if (k) {
-        const unsigned int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fidle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fidle, 0u));
-        if (st == FS_IDLE && np < 0 && rank < k) {
-          volatile int* q = &fh_q[(fh_head + rank) & 255u];
-#ifdef RT_CHECK
-          int spins = 0;
-#endif
-          // (the producer reserved this entry and writes it next: a resident wave of this block)
-          while ((np = *q) < 0) {
-            __builtin_amdgcn_s_sleep(1);
-#ifdef RT_CHECK
-            if (++spins == (1 << 20)) printf("[rt check] hand-off entry %u not written\n", (fh_head + rank) & 255u);
-#endif
-          }
-          *q = -1;
-        }
-        fh_head += k;
-      }
-    }
-    if (np >= 0) {
-      path = np;
-      const uint32_t flags = S.s5[path].y & 0xffu;
-      st = FS_TRACE;  // a listed path always has a ray queued (wf_shade's keep)
-      begin_rays((flags & PF_SHADOW) != 0, (flags & PF_CONT) != 0);
-    }
 #if RT_FINISH_COOP
-    // (with hand-offs: the other waves hand their last paths to the collector, which moves to
-    // quads once it holds every path the block has left)
-    if (WIDE && coop == 0 && drained && (!RT_FINISH_HAND || collector)) {
+    if (WIDE && coop == 0 && drained) {
       // paths left: one per lane
       const unsigned long long live = __ballot(st != FS_IDLE);
       const int nl = __popcll(live);
-      if (nl > 0 && nl <= RT_FINISH_COOP && (!RT_FINISH_HAND || nl == *(volatile int*)&fh_out)) {
+      if (nl > 0 && nl <= RT_FINISH_COOP) {
         // the g-th path moves to lanes 4g .. 4g+3
         const int src = coop_move<4>(L, TS, live, lane, P.stack_cap);
         const int g = lane / 4;
@@ -2411,14 +2355,7 @@ void wf_finish(const WFParams W) {
       }
     }
 #endif
-    if (!__any(st != FS_IDLE)) {
-      if (!collector) break;
-      // the collector stays until the block has no path left (drained: nothing left to claim)
-      if (drained && *(volatile int*)&fh_out == 0) break;
-      // (no lane is tracing or waiting for a shade step: the body below falls through to the
-      // next pick-up; a `continue` here cost the kernel 100 B of scratch)
-      if (*(volatile unsigned int*)&fh_tail == fh_head) __builtin_amdgcn_s_sleep(2);
-    }
+    if (!__any(st != FS_IDLE)) break;
     {  // fuller waves issue first (s_setprio by the lanes holding a path; see RT_FINISH_PRIO)
       const int busy = __popcll(__ballot(st != FS_IDLE));
       if (busy > RT_FINISH_PRIO) __builtin_amdgcn_s_setprio(3);
@@ -2455,8 +2392,6 @@ void wf_finish(const WFParams W) {
       prof_sh++;
 #endif
       const bool sh = st == FS_SHADE;
-      if (RT_FINISH_HAND && !collector && drained && !handing && __popcll(__ballot(st != FS_IDLE)) <= RT_FINISH_HAND)
-        handing = true;
       // the shade step reads its parameters through an opaque copy of the kernel-argument address,
       // so their ~30 pointers are loaded here (scalar loads) instead of being held in SGPRs
       // across the trace loop
@@ -2469,33 +2404,14 @@ void wf_finish(const WFParams W) {
       unsigned long long ns = 0;  // (a coop group runs its path's shade step on all its lanes: counted once)
       const ShadeOut o = shade_path<BSDF, true>(*Wl, EL, path, sh, false, true, ns);
       if (lead()) nsamples += ns;
-      bool ended = false, give = false;
       if (sh) {
         if (lead()) nsteps++;
         if (o.qShadow || o.qCont) {
-          if (RT_FINISH_HAND && handing) {
-            give = true;
-            st = FS_IDLE;
-          } else {
-            st = FS_TRACE;
-            begin_rays(o.qShadow, o.qCont);
-          }
+          st = FS_TRACE;
+          begin_rays(o.qShadow, o.qCont);
         } else {
           st = FS_IDLE;
-          ended = true;
         }
-      }
-      if (RT_FINISH_HAND) {
-        const unsigned long long ge = __ballot(give), ee = __ballot(ended && lead());
-        if (ge) {
-          __threadfence_block();  // this lane's path-state rows before its index is published
-          unsigned int b = 0;
-          if (lane == 0) b = atomicAdd(&fh_tail, (unsigned int)__popcll(ge));
-          b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
-          const unsigned int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(ge >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ge, 0u));
-          if (give) *(volatile int*)&fh_q[(b + r) & 255u] = path;
-        }
-        if (ee && lane == 0) atomicSub(&fh_out, (int)__popcll(ee));
       }
 #ifdef RT_FINISH_PROF
       prof_sh_t += wall_clock64() - ts;
