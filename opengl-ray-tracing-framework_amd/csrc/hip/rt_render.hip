@@ -19,10 +19,6 @@
 #include "rt_abi.h"
 #include "rt_kernels.h"
 #include "rt_wavefront.h"
-
-#ifndef RT_PKT_PASSES  // bulk passes traced by the packet traversal (bit p = pass p; round 6)
-#define RT_PKT_PASSES 0
-#endif
 #include "tri_filter.h"
 
 using rtd::GNode;
@@ -104,7 +100,6 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
-  int pkt_passes = 0;  // bulk passes (bit p = pass p) traced by wf_trace_pkt (packet traversal)
   // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table;
   // ft[0] for batched calls, ft[1 + p] for pipelined one-frame calls on pipeline set p
   struct FrameTable {
@@ -607,8 +602,6 @@ int occupancy(rt_ctx* c) {
   if (const char* e = knob("RT_LDS_STACK")) kl = atoi(e);
   kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;
-  c->pkt_passes = RT_PKT_PASSES;
-  if (const char* e = knob("RT_PKT_PASSES")) c->pkt_passes = (int)strtol(e, nullptr, 0);
   c->trace_lds = kl * 256 * 8;
   bpc = 0;
   // persistent grids: as many blocks as can be resident (the camera pass's instantiation and the
@@ -695,15 +688,6 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
       hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true>), grid, dim3(256), c->trace_lds, st, WP);
     else
       hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
-    return;
-  }
-  if (WIDE && ((c->pkt_passes >> (WP.cam_n ? 0 : WP.pass)) & 1)) {  // packet traversal (wf_trace_pkt)
-    if (WP.cam_n)
-      hipLaunchKernelGGL((rtd::wf_trace_pkt<COUNT, true, false>), grid, dim3(256), c->trace_lds, st, WP);
-    else if (p1)
-      hipLaunchKernelGGL((rtd::wf_trace_pkt<COUNT, false, true>), grid, dim3(256), c->trace_lds, st, WP);
-    else
-      hipLaunchKernelGGL((rtd::wf_trace_pkt<COUNT, false, false>), grid, dim3(256), c->trace_lds, st, WP);
     return;
   }
   if (WP.cam_n)

@@ -1335,290 +1335,6 @@ void wf_trace(const WFParams W) {
   }
 }
 
-// ----------------------------------------------------------------------------- packet trace
-// Wave-coherent traversal: the 64 rays of a wave traverse the 4-wide tree
-// together, one node at a time.  Pixel-major slots make a camera-pass wave one pixel's frames (the
-// same ray 64 times, R6) and a pass-1 wave mostly one pixel's continuations (one origin, one narrow
-// lobe) or shadow rays, so the rays of a wave visit nearly the same nodes; the per-lane dual
-// cursor runs them at half-empty lane utilisation (0.46-0.58 in passes 0-1).  Here:
-//  - the node and triangle records are read by scalar loads (one wave-uniform address) into SGPRs;
-//  - every lane tests the node's four child boxes against its own ray, with its own cull limit;
-//    a child is entered if any lane hits it (ballot), in the entry order of the first lane that
-//    hits any; the stack is wave-uniform, each lane storing its own entry distance per entry (NaN:
-//    its ray missed that box), so a popped subtree is visited by the lanes whose ray hit it and
-//    whose best hit does not cull it (tl_pop's rule, per lane);
-//  - a leaf's triangles are tested only by the lanes whose ray hits the leaf's own box (the
-//    reference leaf box, bit for bit), with tl_triangle_calc's exact test and tie rule.
-// So every lane tests exactly the leaves the per-lane traversal may test (those whose box and
-// every box above it the ray hits: a (grand)child box is hit only if its parent's is)
-// and the closest hit is the same, in any visit order (exact ties by tie_wins).  Lanes whose ray
-// misses a subtree idle through it; the packet ends when the wave's stack is empty.
-typedef const __attribute__((address_space(4))) nt_f4* cf4p;  // constant address space: scalar loads
-template <class T>
-RTD T sld(const void* base, uint32_t byte_off);  // byte_off wave-uniform: s_load from the scalar cache
-template <>
-RTD float4 sld<float4>(const void* base, uint32_t byte_off) {
-  const nt_f4 v = *(cf4p)((const char*)base + byte_off);
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-template <>
-RTD int4 sld<int4>(const void* base, uint32_t byte_off) {
-  const nt_f4 v = *(cf4p)((const char*)base + byte_off);
-  return make_int4(__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w));
-}
-RTD int pkt_key(float f) {  // float order as signed ints (not NaN)
-  const int b = __float_as_int(f);
-  return b >= 0 ? b : (b ^ 0x7fffffff);
-}
-
-// one packet: the lanes with `have` hold started rays (tl_start); on return each holds its result
-template <bool COUNT>
-RTD void pkt_trace(const KParams& P, TraceLane& L, const TraceStack& TS, bool cull, bool have,
-                   unsigned long long& v_int, unsigned long long& v_leaf, unsigned long long& v_tri,
-                   unsigned long long& v_itN, unsigned long long& v_itT) {
-  bool done = !have;  // any-hit found (or no ray)
-  const unsigned long long live = __ballot(have);
-  const unsigned long long bx = __ballot(have && L.ix > 0.0f), by = __ballot(have && L.iy > 0.0f),
-                           bz = __ballot(have && L.iz > 0.0f);
-  // one octant and finite 1/d for every ray: the near / far planes of each axis are wave-uniform
-  const bool uni = __ballot(have && !L.finite) == 0ull && (bx == 0ull || bx == live) && (by == 0ull || by == live) &&
-                   (bz == 0ull || bz == live);
-  const uint32_t oNx = bx ? 0u : 48u, oNy = by ? 16u : 64u, oNz = bz ? 32u : 80u;
-  const float QNAN = __int_as_float(0x7fc00000);
-  int cur = P.qroot;  // wave-uniform
-  bool act = have;    // this lane's ray enters `cur`
-  L.sp = 0;
-  while (true) {
-    if (ref_is_leaf(cur)) {  // the leaf's triangles, for the lanes whose ray hits its box
-      if (COUNT) { v_leaf += act && !done; }
-      const int first = leaf_first(cur), end = first + leaf_count(cur);
-      for (int i = first; i < end; i++) {
-        if (!__ballot(act && !done)) break;
-        if (COUNT) { v_itT++; v_tri += act && !done; }
-        const uint32_t off = (uint32_t)i * 48u;
-        const float4 A = sld<float4>(P.trx, off), B = sld<float4>(P.trx, off + 16u), Cc = sld<float4>(P.trx, off + 32u);
-        if (act && !done && tl_triangle_calc<true>(P, L, i, A, B, Cc) && L.anyhit) done = true;
-      }
-    } else {  // a 4-wide node
-      if (COUNT) { v_itN++; v_int += act && !done; }
-      const uint32_t off = (uint32_t)cur << 7;
-      const int4 rf = sld<int4>(P.qnodes, off + 96u);
-      const float lim = cull ? L.lim : __int_as_float(0x7f800000);
-      const bool on = act && !done;
-      float t0[4], t1[4];
-      if (uni) {
-        const float4 nx = sld<float4>(P.qnodes, off + oNx), ny = sld<float4>(P.qnodes, off + oNy),
-                     nz = sld<float4>(P.qnodes, off + oNz);
-        const float4 fx = sld<float4>(P.qnodes, off + (48u - oNx)), fy = sld<float4>(P.qnodes, off + (80u - oNy)),
-                     fz = sld<float4>(P.qnodes, off + (112u - oNz));
-        tl_qnode_t01(L, nx, ny, nz, fx, fy, fz, t0, t1);
-      } else {  // the literal slab of RT:309-313 per lane (equal to the plane choice for finite 1/d)
-        const float4 lx = sld<float4>(P.qnodes, off), ly = sld<float4>(P.qnodes, off + 16u),
-                     lz = sld<float4>(P.qnodes, off + 32u), hx = sld<float4>(P.qnodes, off + 48u),
-                     hy = sld<float4>(P.qnodes, off + 64u), hz = sld<float4>(P.qnodes, off + 80u);
-        auto generic = [&](int c, float ax, float ay, float az, float cx, float cy, float cz) {
-          const f3 f = (mk3(cx, cy, cz) - L.o()) * L.inv();
-          const f3 n = (mk3(ax, ay, az) - L.o()) * L.inv();
-          t0[c] = max_(min_(f.x, n.x), max_(min_(f.y, n.y), min_(f.z, n.z)));
-          t1[c] = min_(max_(f.x, n.x), min_(max_(f.y, n.y), max_(f.z, n.z)));
-        };
-        generic(0, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x);
-        generic(1, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y);
-        generic(2, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z);
-        generic(3, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w);
-      }
-      const int rr[4] = {rf.x, rf.y, rf.z, rf.w};
-      float k[4];
-      unsigned long long m[4];
-      int okb = 0;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const bool ok = on && rr[c] != Q_EMPTY && t1[c] >= t0[c] && t1[c] > 0.0f && !(t0[c] > lim);
-        k[c] = ok ? t0[c] : QNAN;
-        okb |= (int)ok << c;
-        m[c] = __ballot(ok);
-      }
-      const unsigned long long any = m[0] | m[1] | m[2] | m[3];
-      if (any) {
-        // entry order of the first lane that hits a child; children only other lanes hit go last
-        const int lead = (int)__builtin_ctzll(any);
-        int key[4], ord[4] = {0, 1, 2, 3};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const float kl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(k[c]), lead));
-          key[c] = !m[c] ? 0x7fffffff : (kl == kl ? pkt_key(kl) : 0x7ffffffe);
-        }
-#define RT_PSWAP(a, b)                                                         \
-  {                                                                            \
-    const bool sw = key[b] < key[a] || (key[b] == key[a] && ord[b] < ord[a]); \
-    const int tk = sw ? key[b] : key[a], to = sw ? ord[b] : ord[a];            \
-    key[b] = sw ? key[a] : key[b]; ord[b] = sw ? ord[a] : ord[b];              \
-    key[a] = tk; ord[a] = to;                                                  \
-  }
-        RT_PSWAP(0, 1) RT_PSWAP(2, 3) RT_PSWAP(0, 2) RT_PSWAP(1, 3) RT_PSWAP(1, 2)
-#undef RT_PSWAP
-        const int n = (m[0] != 0ull) + (m[1] != 0ull) + (m[2] != 0ull) + (m[3] != 0ull);
-        // far to near: every lane pushes its own entry distance (NaN: its ray missed the box)
-#pragma unroll
-        for (int j = 3; j >= 1; j--) {
-          if (j >= n) continue;  // (wave-uniform; static indices keep ord / k / rr in registers)
-          const int c = ord[j];
-          const float kc = c == 0 ? k[0] : c == 1 ? k[1] : c == 2 ? k[2] : k[3];
-          tl_push(L, TS, make_int2(c == 0 ? rr[0] : c == 1 ? rr[1] : c == 2 ? rr[2] : rr[3], __float_as_int(kc)));
-        }
-        const int c0 = ord[0];
-        cur = c0 == 0 ? rr[0] : c0 == 1 ? rr[1] : c0 == 2 ? rr[2] : rr[3];
-        act = ((okb >> c0) & 1) != 0;
-        continue;
-      }
-    }
-    // pop the next subtree some lane still enters (tl_pop's cull rule, per lane)
-    bool found = false;
-    while (L.sp > 0 && __ballot(!done)) {
-      --L.sp;
-      const int2 ent = L.sp < TS.KL ? TS.lds[L.sp * TL_LANES] : unpack_ent(*TS.ovf_at(L.sp));
-      const float key = __int_as_float(ent.y);
-      act = !done && key == key && !(cull && key > L.lim);
-      if (__ballot(act)) {
-        cur = __builtin_amdgcn_readfirstlane(ent.x);
-        found = true;
-        break;
-      }
-    }
-    if (!found) break;
-  }
-}
-
-#ifndef RT_PKT_WPE  // waves per SIMD of the packet trace
-#define RT_PKT_WPE 8
-#endif
-template <bool COUNT, bool CAM, bool P1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PKT_WPE)))
-void wf_trace_pkt(const WFParams W) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const KParams& P = W.K;
-  const WFState& S = W.S;
-  const int qin = W.pass & 1;
-  const unsigned int nq = CAM ? W.cam_n : S.cnt[cq(qin)];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
-    S.cnt[cq(qin ^ 1)] = 0u;
-    S.cnt[ca(qin ^ 1)] = 0u;
-  }
-  if (nq == 0u || !P.has_scene) {
-    if (!P.has_scene) {
-      for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
-        const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
-        S.res[e] = -1;
-      }
-    }
-    return;
-  }
-  TraceStack TS;
-  TS.KL = P.lds_entries;
-#ifdef RT_CHECK
-  TS.cap = P.stack_cap;
-#endif
-  TS.lds0 = reinterpret_cast<int2*>(smem);
-  TS.lds = TS.lds0 + threadIdx.x;
-  TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
-  TS.ovs = P.ovf_lanes;
-  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
-  const int lane = (int)(threadIdx.x & 63);
-  // claims as in wf_trace's bulk passes: 8 queue segments, guided chunk sizes (wave-uniform)
-  unsigned int pool_next = 0, pool_end = 0;
-  const unsigned int wave_id = blockIdx.x * (TL_LANES / 64) + (threadIdx.x >> 6);
-  const unsigned int part_waves = min(gridDim.x * (TL_LANES / 64), (nq + RT_TAIL_CHUNK - 1u) / RT_TAIL_CHUNK);
-  bool drained = wave_id >= part_waves;
-  unsigned int seg = blockIdx.x & 7u, seg_tries = 0, seg_seen = 0;
-  const unsigned int seg_waves = max(1u, part_waves / 8u);
-  TraceLane L;
-  L.ox = L.oy = L.oz = L.dx = L.dy = L.dz = L.ix = L.iy = L.iz = 0.0f;
-  L.best = INF; L.bestt = 0.0f; L.besttri = -1; L.lim = INF;
-  L.sp = L.cur = L.tri_i = L.tri_end = 0;
-  L.haveCur = L.anyhit = L.finite = false;
-  L.offNx = L.offNy = L.offNz = 0;
-  unsigned long long v_int = 0, v_leaf = 0, v_tri = 0, v_itN = 0, v_itT = 0;
-  while (!drained) {
-    if (pool_next >= pool_end) {
-      while (true) {  // (wave-uniform)
-        const unsigned int lo = (unsigned int)((unsigned long long)nq * seg / 8u);
-        const unsigned int hi = (unsigned int)((unsigned long long)nq * (seg + 1u) / 8u);
-        const unsigned int left = hi - min(max(seg_seen, lo), hi);
-        const unsigned int chunk = min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (seg_waves * RT_GUIDED)) & ~63u));
-        unsigned int b = 0;
-        if (lane == 0) b = atomicAdd(&S.cnt[xcnt(seg)], chunk);
-        b = lo + __builtin_amdgcn_readfirstlane(__shfl(b, 0));
-        if (b < hi) {
-          pool_next = b;
-          pool_end = min(b + chunk, hi);
-          seg_seen = pool_end;
-          break;
-        }
-        if (++seg_tries >= 8u) {
-          drained = true;
-          break;
-        }
-        seg = (seg + 1u) & 7u;
-        seg_seen = 0xFFFFFFFFu;
-      }
-      if (drained) break;
-    }
-    // the next (up to) 64 rays of the pool, one per lane
-    const unsigned int nr = min(64u, pool_end - pool_next);
-    const bool have = (unsigned int)lane < nr;
-    int entry = 0;
-    if (have) {
-      const unsigned int qi = pool_next + (unsigned int)lane;
-      if (CAM) {
-        entry = (int)(qi << 1);
-        L.anyhit = false;
-        uint32_t seed_unused, frame_unused;
-        const f3 d = camera_ray(P, S, qi, seed_unused, frame_unused);
-        L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
-        L.dx = d.x; L.dy = d.y; L.dz = d.z;
-      } else {
-        entry = S.queue[qin][qi];
-        const int path = entry >> 1;
-        L.anyhit = (entry & 1) != 0;
-        const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
-        if (P1) {
-          p1_ray(S, (unsigned)W.n_frames, (unsigned)path, oa, L.ox, L.oy, L.oz);
-          L.dx = oa.x; L.dy = oa.y; L.dz = oa.z;
-        } else {
-          const float2 ob = L.anyhit ? S.sb[path] : S.rb[path];
-          L.ox = oa.x; L.oy = oa.y; L.oz = oa.z;
-          L.dx = oa.w; L.dy = ob.x; L.dz = ob.y;
-        }
-      }
-      tl_start<true>(P, L);
-    }
-    pool_next += nr;
-    pkt_trace<COUNT>(P, L, TS, cull, have, v_int, v_leaf, v_tri, v_itN, v_itT);
-    if (have) {
-      if (RT_RES_NT) __builtin_nontemporal_store(L.besttri, &S.res[entry]);
-      else S.res[entry] = L.besttri;
-    }
-  }
-  if (COUNT) {  // the same counters as wf_trace's COUNT build (RT_DEBUG_PASSES): node-phase iterations
-                // and lane-sums, triangle-phase iterations and lane-sums
-    for (int off = 32; off > 0; off >>= 1) {
-      v_int += __shfl_xor(v_int, off);
-      v_leaf += __shfl_xor(v_leaf, off);
-      v_tri += __shfl_xor(v_tri, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&P.stats[8], v_itN);
-      atomicAdd(&P.stats[9], v_int);
-      atomicAdd(&P.stats[10], v_itT);
-      atomicAdd(&P.stats[11], v_tri);
-      atomicAdd(&P.stats[2], v_int);
-      atomicAdd(&P.stats[3], v_leaf);
-      atomicAdd(&P.stats[4], v_tri);
-      atomicAdd(&P.stats[5], v_itN + v_itT);
-    }
-  }
-}
-
 // ----------------------------------------------------------------------------- shade
 // Paths per block-iteration of wf_shade = 256 x SH_SUB: the block stages its queue / active
 // entries in LDS and claims global space with one atomic per list per block-iteration.
