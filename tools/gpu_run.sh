@@ -14,7 +14,8 @@
 #   ab4=<v>,<v>,...         C4 256-frame calls
 #   single=<v>,<v>,...      C3 one-frame calls (tools/ab_single.py)
 #   rank=<spec> ...         N = 8 rank shares on one GPU (tools/rank_sim.py); spec: VAR=v,VAR=v or "-"
-#   passes=<config>:<frames>  per-pass times and counts of one frame group (dev library)
+#   passes=<cfg>:<frames>[:VAR=v;VAR=v][:count]  per-pass times (or visit counts) of one frame group
+#                           (dev library)
 #   bench[=<bench.py args>] the driver's bench command (default args: --gpus 1 --steps 20 --warmup 5)
 #   configs                 bench lines of C2, C4, C5 (256-frame steps)
 #   evidence[=<tag>]        round evidence: tests, rocprofv3 trace + PMC summary, bench, interactive
@@ -64,10 +65,11 @@ for step in "$@"; do
       env "${envs[@]}" RTAMD_LIB=$PWD/opengl-ray-tracing-framework_amd/lib/librtamd_dev.so timeout -k 10 600 \
         python3 tools/rank_sim.py --worlds ${WORLDS:-1,8} --assign ${ASSIGN:-balanced} --reps 2 --out $O/rank_$name.jsonl > $L 2>&1 || fail $step $? $L
       python3 -c "import sys,json; [print(' ', d['world'], d['assign'], d['max_ms'], d['mean_ms'], d['imbalance'], d['efficiency_vs_n1']) for d in map(json.loads, open(sys.argv[1]))]" $O/rank_$name.jsonl ;;
-    passes)
-      cfg=${arg%%:*}; fr=${arg#*:}
-      RT_DEBUG_PASSES=1 RT_GROUPS=1 RTAMD_LIB=$PWD/opengl-ray-tracing-framework_amd/lib/librtamd_dev.so timeout -k 10 300 \
-        python3 -u tools/pass_counts.py --config $cfg --frames $fr --max-paths $((fr * 1920 * 1080)) > $L 2>&1 || fail $step $? $L
+    passes)  # passes=<config>:<frames>[:VAR=v;VAR=v][:count]
+      IFS=':' read -r cfg fr penv pcount <<< "$arg"
+      envs=(); [ -n "$penv" ] && IFS=';' read -ra envs <<< "$penv"
+      env "${envs[@]}" RT_DEBUG_PASSES=1 RT_GROUPS=1 timeout -k 10 300 \
+        python3 -u tools/pass_counts.py --config $cfg --frames $fr --max-paths $((fr * 1920 * 1080)) ${pcount:+--count} > $L 2>&1 || fail $step $? $L
       grep -a "\] group\|pass" $L | head -30 ;;
     bench)
       timeout -k 10 600 python3 bench.py ${arg:---gpus 1 --steps 20 --warmup 5} > $O/bench.json 2> $L || fail $step $? $L
