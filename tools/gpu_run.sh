@@ -20,6 +20,8 @@
 #   configs                 bench lines of C2, C4, C5 (256-frame steps)
 #   evidence[=<tag>]        round evidence: tests, rocprofv3 trace + PMC summary, bench, interactive
 #                           (tools/round_gpu.sh)
+#   profile_configs=<round> C4 / C5 rocprofv3 trace + PMC summaries and bench lines
+#                           (tools/profile_configs.sh), then the C2 bench line
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:?usage: gpu_run.sh <tag> <step> ...}; shift
@@ -82,6 +84,11 @@ for step in "$@"; do
     evidence)
       TAG=${arg:-r06_C3} bash tools/round_gpu.sh > $L 2>&1 || fail $step $? $L
       tail -20 $L ;;
+    profile_configs)
+      bash tools/profile_configs.sh ${arg:-r06} > $L 2>&1 || fail $step $? $L
+      grep -E "^C[45] " $L
+      timeout -k 10 300 python3 bench.py --config C2 --frames-per-step 256 --steps 3 --warmup 1 > gpurun_out/profiles/${arg:-r06}_bench_C2.json 2>> $L || fail $step $? $L
+      python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print('C2', d['value'], d['ms_per_frame'], d.get('ms_single_frame_latency'), d.get('ms_per_frame_single'))" gpurun_out/profiles/${arg:-r06}_bench_C2.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
