@@ -140,8 +140,9 @@ def test_roofline_bound_follows_the_limiter():
 def _committed_bench_line(config="C3"):
     """the newest committed bench line of a configuration in the round-4 roofline format (with a
     PMC profile), and its profile"""
-    pat = "r*_bench_C3.json" if config == "C3" else f"r*_other_configs/bench_{config}.json"
-    for p in sorted((ROOT / "profiles").glob(pat), reverse=True):
+    prof = ROOT / "profiles"
+    found = list(prof.glob(f"r*_bench_{config}.json")) + list(prof.glob(f"r*_other_configs/bench_{config}.json"))
+    for p in sorted(found, key=lambda q: str(q.relative_to(prof)), reverse=True):
         d = json.loads(p.read_text())
         if "avg_launch_ms_regime" in d.get("roofline", {}) and d["roofline"].get("profile"):
             return p, d
