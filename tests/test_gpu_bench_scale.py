@@ -131,8 +131,10 @@ def test_bench_step_full_scale_matches_oracle_windows(env_maps, bench_inputs):
     img, st, n_local = _render_bench_shape(sd, env_maps, fp, ro, hist, tile, 0, 1, None)
     # the bench's shape: two 512-frame launches (206 GB of path state each), 2 frame groups of
     # 256 frames x 9 passes, all on the bulk kernels (no finisher), every pixel-frame sampled
-    assert st["launches"] == 2, st
-    assert st["trace_launches"] == 2 * 2 * 9, st
+    # (a box with less free HBM halves the frames per launch again: still >= 64 frames per group,
+    # the bulk kernels and the camera records)
+    assert st["launches"] in (2, 4), st
+    assert st["trace_launches"] == st["launches"] * 2 * 9, st
     assert st["finish_steps"] == 0
     assert st["samples"] == W * H * N_FRAMES
     rays_per_sample = st["rays"] / st["samples"]
@@ -155,8 +157,8 @@ def test_bench_rank_share_n8_matches_oracle_windows(env_maps, bench_inputs):
     mine = tiling.local_tiles(W, H, tile, tile, rank, world, owner)
     assert n_local == len(mine)
     # one launch holds the whole 1024-frame step (51 GB of path state): two groups of 512
-    assert st["launches"] == 1, st
-    assert st["trace_launches"] == 2 * 9, st
+    assert st["launches"] in (1, 2), st
+    assert st["trace_launches"] == st["launches"] * 2 * 9, st
     assert st["finish_steps"] == 0
     npx = sum(tiling.tile_rect(t, W, H, tile, tile)[2] * tiling.tile_rect(t, W, H, tile, tile)[3] for t in mine)
     assert st["samples"] == npx * N_FRAMES
