@@ -109,7 +109,7 @@ def bench_inputs(env_maps):
     return sd, fp, ro, frames, hist
 
 
-def _check(img, sd, env, frames, hist, windows, owned=None):
+def _check(img, sd, env, frames, hist, windows):
     assert len(windows) >= 12
     ref = _oracle_windows(sd, env, frames, hist, windows)
     bad = []
