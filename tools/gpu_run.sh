@@ -65,7 +65,7 @@ for step in "$@"; do
       name=$(echo "${arg:--}" | tr ',=' '_-')
       envs=(); [ "${arg:--}" != "-" ] && IFS=',' read -ra envs <<< "$arg"
       env "${envs[@]}" RTAMD_LIB=$PWD/opengl-ray-tracing-framework_amd/lib/librtamd_dev.so timeout -k 10 600 \
-        python3 tools/rank_sim.py --worlds ${WORLDS:-1,8} --assign ${ASSIGN:-balanced} --reps 2 --out $O/rank_$name.jsonl > $L 2>&1 || fail $step $? $L
+        python3 tools/rank_sim.py --worlds ${WORLDS:-1,8} --assign ${ASSIGN:-balanced} --tile ${TILE:-16} --reps 2 --out $O/rank_$name.jsonl > $L 2>&1 || fail $step $? $L
       python3 -c "import sys,json; [print(' ', d['world'], d['assign'], d['max_ms'], d['mean_ms'], d['imbalance'], d['efficiency_vs_n1']) for d in map(json.loads, open(sys.argv[1]))]" $O/rank_$name.jsonl ;;
     passes)  # passes=<config>:<frames>[:VAR=v;VAR=v][:count]
       IFS=':' read -r cfg fr penv pcount <<< "$arg"
