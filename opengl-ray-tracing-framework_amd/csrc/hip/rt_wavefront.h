@@ -1017,8 +1017,11 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // the last grid lanes x RT_TAIL_FACTOR rays, then RT_TAIL_CHUNK).  A late 1024-ray claim of one
                    // costly pixel run held a wave long after the others had drained.  With one counter, C3 bulk
                    // 1 / 2 / 3 / 4: +0.49 / +0.88, +1.04 / +0.32 / -0.07%; N=8 rank shares 70.9 -> 69.9 ms (round 5,
-                   // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep static shares + 64-ray claims
-#define RT_GUIDED 2u
+                   // profiles/r05_ab_bulk_guided_claims_C3.log); one-frame passes keep static shares + 64-ray claims.
+                   // Round 6, with a new segment's first claim tail-sized: 3 vs 2 at N = 1 +0.00% (5 rounds,
+                   // profiles/r06_ab_guided3_C3.log), N = 8 slowest rank 65.8 -> 65.1 / 65.4 ms (4: 65.4 / 65.5;
+                   // profiles/r06_rank_ab_claim_knobs_C3.log)
+#define RT_GUIDED 3u
 #endif
 #ifndef RT_REFILL_MIN_SMALL  // the small passes' refill threshold: C3 1080p one-frame calls 4 / 6 / 8 / 12 / 16 vs 20:
                              // -0.5 / -0.7 / -1.1, -0.6 / -0.9, -0.5 / -0.7% back-to-back (round 5,
