@@ -19,6 +19,10 @@
 #include "rt_abi.h"
 #include "rt_kernels.h"
 #include "rt_wavefront.h"
+
+#ifndef RT_SPLIT_KINDS  // bulk groups trace shadow rays and continuations in launches of their own (round 6)
+#define RT_SPLIT_KINDS 1
+#endif
 #include "tri_filter.h"
 
 using rtd::GNode;
@@ -100,6 +104,7 @@ struct rt_ctx {
   int blocks_per_cu = 0, block_lds = 0;      // megakernel
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
+  int split_kinds = RT_SPLIT_KINDS;  // bulk groups: shadow rays and continuations in queues of their own
   // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table;
   // ft[0] for batched calls, ft[1 + p] for pipelined one-frame calls on pipeline set p
   struct FrameTable {
@@ -600,6 +605,7 @@ int occupancy(rt_ctx* c) {
   // wavefront traversal: short LDS stack + global overflow
   int kl = 8;  // 16 KiB per block: LDS leaves room for 8 waves/SIMD (12 entries: 6; C3 5853 -> 5959 at 10, 6155 at 8 with the dual schedule at 8 waves)
   if (const char* e = knob("RT_LDS_STACK")) kl = atoi(e);
+  if (const char* e = knob("RT_SPLIT_KINDS")) c->split_kinds = atoi(e);
   kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
@@ -688,6 +694,16 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
       hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true, true>), grid, dim3(256), c->trace_lds, st, WP);
     else
       hipLaunchKernelGGL((rtd::wf_trace<false, true, false, true>), grid, dim3(256), c->trace_lds, st, WP);
+    return;
+  }
+  if (WP.split && !WP.cam_n && !COUNT && WIDE) {  // split queues: the shadow rays, then the continuations
+    if (p1) {
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 2>), grid, dim3(256), c->trace_lds, st, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 1>), grid, dim3(256), c->trace_lds, st, WP);
+    } else {
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 2>), grid, dim3(256), c->trace_lds, st, WP);
+      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 1>), grid, dim3(256), c->trace_lds, st, WP);
+    }
     return;
   }
   if (WP.cam_n)
@@ -843,6 +859,7 @@ int alloc_wavefront(rt_ctx* c, size_t paths) {
     w.res = (int*)carve(P * 8);
     w.fin = (float4*)carve(P * 16);
     w.queue[0] = (int*)carve(P * 8); w.queue[1] = (int*)carve(P * 8);
+    w.queue_s[0] = w.queue[0] + P; w.queue_s[1] = w.queue[1] + P;  // (split queues: one entry per path each)
     w.active[0] = (int*)carve(P * 4); w.active[1] = (int*)carve(P * 4);
     w.cnt = (unsigned int*)carve(rtd::kCntWords * 4);
   }
@@ -1608,6 +1625,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         // (not for frame groups of one frame each: their blends must run in frame order)
         WP.fuse_blend = (!pipe && WP.n_frames == 1 && (pix_split || G == 1) && !count) ? 1 : 0;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
+        // bulk groups (the wf_shade<..., SH_SUB_BULK / CAM> launches) queue the two ray kinds apart
+        WP.split = (c->split_kinds && c->wide && !count && !c->tile_cost_on && slots_g[g] > c->finish_slots && !WP.fuse_blend) ? 1 : 0;
         sg[g] = pipe ? ps : g == 0 ? c->stream : c->aux[g];
       }
       // camera directions of this call's pixels (every group reads them)
@@ -1733,12 +1752,13 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
 #ifdef RT_DEV
           if (debug_passes) {  // development aid: per-pass rays / visits / duration (syncs!)
             unsigned long long h[16];
-            unsigned int q[2];
+            unsigned int q[8];
             HIPCHK(c, hipStreamSynchronize(sg[g]));
             float ms = 0.0f;
             HIPCHK(c, hipEventElapsedTime(&ms, t0, t1));
             HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-            HIPCHK(c, hipMemcpy(q, WP.S.cnt + rtd::cq(pass & 1), 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(q, WP.S.cnt, sizeof(q), hipMemcpyDeviceToHost));
+            q[0] = q[rtd::cq(pass & 1)] + (WP.split ? q[rtd::cqs(pass & 1)] : 0u);  // (split queues: both kinds)
             fprintf(stderr, "[rt] group %d pass %d: %u rays %.3f ms  cum internal %llu leaf %llu tri %llu iters %llu "
                     "wave-iters max %llu ray-steps max %llu\n", g, pass, (WP.cam_n ? WP.cam_n : q[0]), ms, h[2], h[3], h[4], h[5], h[6], h[7]);
             unsigned long long hq[6];

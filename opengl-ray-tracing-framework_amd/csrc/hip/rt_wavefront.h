@@ -67,6 +67,7 @@ struct WFState {
   // medium scattering distance of a continuation, else 0) instead of {o.xyz, d.x} + {d.y, d.z}
   float4* __restrict__ org;
   int* queue[2];                // ray queue entries: path << 1 | is_shadow
+  int* queue_s[2];              // split queues (WFParams::split): the shadow rays, queue[k] + slots
   int* active[2];               // active path ids
   unsigned int* __restrict__ cnt;  // queue counts, active counts, trace fetch, segment claims (cq, ca, ... below)
 };
@@ -83,7 +84,11 @@ __host__ __device__ constexpr unsigned int cq(unsigned int i) { return i; }
 __host__ __device__ constexpr unsigned int ca(unsigned int i) { return 2u + i; }
 constexpr unsigned int kCntFetch = 4u;
 __host__ __device__ constexpr unsigned int xcnt(unsigned int s) { return 160u + 32u * s; }
-constexpr unsigned int kCntWords = 160u + 32u * 8u;
+// split queues (WFParams::split): the shadow-ray queue counts of the two parities, and the claim
+// counters of its 8 segments (the continuation queue keeps cq / xcnt)
+__host__ __device__ constexpr unsigned int cqs(unsigned int i) { return 6u + i; }
+__host__ __device__ constexpr unsigned int xcnts(unsigned int s) { return 416u + 32u * s; }
+constexpr unsigned int kCntWords = 416u + 32u * 8u;
 
 // Per-wave statistics flushes of wf_shade / wf_finish (rays, samples, finisher steps) go to one of
 // kStatShards 128-B lines after the 128 counters (words 0, 1, 2 of shard s = rays, samples, finish
@@ -143,6 +148,9 @@ struct WFParams {
   // per group): a finishing path blends into the accumulation itself (wf_blend's operations,
   // RT:1552) instead of writing fin for a wf_blend launch after the last pass
   int fuse_blend;
+  // bulk groups: the shade queues shadow rays (queue_s, cqs) and continuations (queue, cq) apart,
+  // and each secondary pass traces them in two launches, wf_trace<..., KIND = 2> and <..., 1>
+  int split;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -484,7 +492,10 @@ RTD bool tl_tri_hit(const KParams& P, const TraceLane& L, int i, const float4 A,
   t_out = t;
   return ok & inside;
 }
-template <bool WIDE>
+// AH (the any-hit kernel of split queues, wf_trace<..., KIND = 2>): best is +inf until the hit that
+// ends the ray, so `dist <= best` is the NaN test `t >= 0.0005` already makes and there is no tie;
+// the accepted triangle ends the ray (no culling limit to update)
+template <bool WIDE, bool AH = false>
 RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A, const float4 B, const float4 Cc) {
   // straight-line form: every condition of RT:262-281 folded into one predicate (a 64-lane wave
   // runs the whole test for some lane anyway; early returns, and round 2's rcp-based pre-reject
@@ -495,7 +506,7 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   const float num = dot(ng, p1) - dot(L.o(), ng);
   const float t = num / dot(L.d(), ng);                                // RT:265
   const float dist = t - 0.00001f;
-  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (WIDE ? dist <= L.best : dist < L.best);  // RT:262, 268, 328/356
+  bool ok = !(fabs_(dn) < 0.00001f) & (t >= 0.0005f) & (AH || (WIDE ? dist <= L.best : dist < L.best));  // RT:262, 268, 328/356
   const f3 Pp = L.o() + L.d() * t;
   const float qx = Pp.x - p1.x, qy = Pp.y - p1.y, qz = Pp.z - p1.z;
   const float b2 = __builtin_fmaf(B.x, qx, __builtin_fmaf(B.y, qy, B.z * qz));
@@ -508,6 +519,10 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   bool inside = mn > 0.0f;
   if (ok & !((fabsf(mn) > m) & (m < 0.25f))) inside = tl_edges_exact(P, i, p1, ng, Pp);
   ok &= inside;
+  if (AH) {
+    if (ok) L.besttri = i;
+    return ok;
+  }
   if (WIDE && ok && dist == L.best) ok = L.besttri >= 0 && tie_wins(P, L, i, L.besttri);
   if (ok) {
     L.set_best(dist, P.cull_eps);
@@ -516,11 +531,11 @@ RTD bool tl_triangle_calc(const KParams& P, TraceLane& L, int i, const float4 A,
   }
   return ok;
 }
-template <bool WIDE>
+template <bool WIDE, bool AH = false>
 RTD bool tl_triangle(const KParams& P, TraceLane& L, int i) {
   const uint32_t off = (uint32_t)i * 48u;
   const float4 A = ld<float4>(P.trx, off), B = ld<float4>(P.trx, off + 16u), Cc = ld<float4>(P.trx, off + 32u);
-  return tl_triangle_calc<WIDE>(P, L, i, A, B, Cc);
+  return tl_triangle_calc<WIDE, AH>(P, L, i, A, B, Cc);
 }
 
 RTD void tl_push(TraceLane& L, const TraceStack& S, int2 ent) {
@@ -627,8 +642,20 @@ RTD void tl_qnode_keys(const TraceLane& L, bool cull, float cull_eps, const int4
 }
 // POP: pop the next subtree when no child was entered; without it the caller pops (returns true
 // when it must)
-template <bool POP = true>
+// SORT = false (any-hit rays: the order of the children changes which hit ends the ray, never
+// whether one is found): the lowest hit slot is entered, the others stacked in slot order
+template <bool POP = true, bool SORT = true>
 RTD bool tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool cull, float (&k)[4], int (&r)[4]) {
+  if (!SORT) {
+    const bool v0 = r[0] != Q_EMPTY, v1 = r[1] != Q_EMPTY, v2 = r[2] != Q_EMPTY, v3 = r[3] != Q_EMPTY;
+    if (v3 && (v0 || v1 || v2)) tl_push(L, S, make_int2(r[3], __float_as_int(k[3])));
+    if (v2 && (v0 || v1)) tl_push(L, S, make_int2(r[2], __float_as_int(k[2])));
+    if (v1 && v0) tl_push(L, S, make_int2(r[1], __float_as_int(k[1])));
+    L.cur = v0 ? r[0] : v1 ? r[1] : v2 ? r[2] : r[3];
+    if (!POP) return L.cur == Q_EMPTY;
+    L.haveCur = L.cur != Q_EMPTY || tl_pop(P, L, S, cull);
+    return false;
+  }
   const int n = (r[0] != Q_EMPTY) + (r[1] != Q_EMPTY) + (r[2] != Q_EMPTY) + (r[3] != Q_EMPTY);
   // valid children sort ahead of empty slots unless a valid entry key is +inf (degenerate)
   const bool ordered = !((r[0] != Q_EMPTY && !(k[0] < INFINITY)) || (r[1] != Q_EMPTY && !(k[1] < INFINITY)) ||
@@ -665,7 +692,7 @@ RTD bool tl_qnode_push(const KParams& P, TraceLane& L, const TraceStack& S, bool
   L.haveCur = r[0] != Q_EMPTY || tl_pop(P, L, S, cull);
   return false;
 }
-template <bool POP = true>
+template <bool POP = true, bool SORT = true>
 RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull) {
 #ifdef RT_CHECK
   if ((unsigned)L.cur >= (unsigned)P.n_qnodes) {
@@ -689,7 +716,7 @@ RTD bool tl_qnode(const KParams& P, TraceLane& L, const TraceStack& S, bool cull
                  hy = ld<float4>(P.qnodes, off + 64u), hz = ld<float4>(P.qnodes, off + 80u);
     tl_qnode_keys(L, cull, P.cull_eps, rf, lx, ly, lz, hx, hy, hz, k, r);
   }
-  return tl_qnode_push<POP>(P, L, S, cull, k, r);
+  return tl_qnode_push<POP, SORT>(P, L, S, cull, k, r);
 }
 // the node fetch alone (the finisher issues it before its triangle test): rf + six planes, near /
 // far for a finite 1/d, lo / hi otherwise (tl_start's offsets cover both)
@@ -1023,6 +1050,9 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // profiles/r06_rank_ab_claim_knobs_C3.log)
 #define RT_GUIDED 3u
 #endif
+#ifndef RT_REFILL_MIN_AH  // the any-hit kernel's refill threshold (split queues)
+#define RT_REFILL_MIN_AH RT_REFILL_MIN
+#endif
 #ifndef RT_REFILL_MIN_SMALL  // the small passes' refill threshold: C3 1080p one-frame calls 4 / 6 / 8 / 12 / 16 vs 20:
                              // -0.5 / -0.7 / -1.1, -0.6 / -0.9, -0.5 / -0.7% back-to-back (round 5,
                              // profiles/r05_ab_single_refill_min_small_C3.log; the bulk stays at 20)
@@ -1050,28 +1080,39 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // (scattered 4-B results and 8-B overflow-stack entries, each a partial sector)
 #define RT_RES_NT 1
 #endif
+#ifndef RT_SHADOW_SORT  // the any-hit kernel of split queues sorts children by entry distance (1) or enters
+                        // the lowest hit slot and stacks the rest (0): C3 +1.02% / +2.41% over one queue of
+                        // both kinds (round 6, profiles/r06_ab_split_kinds_C3.log)
+#define RT_SHADOW_SORT 0
+#endif
 #ifndef RT_TRACE_WPE_DUAL  // dual cursor at 8 waves/SIMD (64 VGPRs; its 8-B spill is on the refill path): +2.4%
 #define RT_TRACE_WPE_DUAL 8
 #endif
 // CAM: the implicit camera pass (WFParams::cam_n); a separate instantiation so the secondary
 // passes' kernels carry none of its registers.  STATIC: small groups' static first shares (below;
 // a separate instantiation: the code alone cost the bulk's kernels 0.4%).
-template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false>  // P1: pass 1's 16-B rays
+// KIND: 0 the pass's one queue (both kinds); with split queues (WFParams::split) 1 the
+// continuations (closest hit) and 2 the shadow rays (any hit: no culling, no child sort, AH
+// triangle test), each launch its own instantiation with no per-lane kind
+template <bool COUNT, bool WIDE, bool CAM, bool STATIC = false, bool P1 = false, int KIND = 0>  // P1: pass 1's 16-B rays
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WPE_DUAL)))
 void wf_trace(const WFParams W) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KParams& P = W.K;
   const WFState& S = W.S;
   const int qin = W.pass & 1;
-  const unsigned int nq = CAM ? W.cam_n : S.cnt[cq(qin)];
+  constexpr bool AHK = KIND == 2;  // every ray of the launch is any-hit
+  const unsigned int nq = CAM ? W.cam_n : AHK ? S.cnt[cqs(qin)] : S.cnt[cq(qin)];
+  const int* __restrict__ Q = AHK ? S.queue_s[qin] : S.queue[qin];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shade pass after us appends here
     S.cnt[cq(qin ^ 1)] = 0u;
+    S.cnt[cqs(qin ^ 1)] = 0u;
     S.cnt[ca(qin ^ 1)] = 0u;
   }
   if (nq == 0u || !P.has_scene) {
     if (!P.has_scene) {  // empty scene: every ray misses (RT:346 reads a zero node)
       for (unsigned int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
-        const int e = CAM ? (int)(i << 1) : S.queue[qin][i];
+        const int e = CAM ? (int)(i << 1) : Q[i];
         S.res[e] = -1;
       }
     }
@@ -1089,7 +1130,8 @@ void wf_trace(const WFParams W) {
   TS.lds = TS.lds0 + threadIdx.x;
   TS.ovf = (gu64*)(P.stack_ovf) + blockIdx.x * TL_LANES;
   TS.ovs = P.ovf_lanes;
-  const bool cull = (P.flags & RT_FLAG_NO_CULL) == 0;
+  // (an any-hit ray's best is +inf until the hit that ends it: nothing to cull)
+  const bool cull = !AHK && (P.flags & RT_FLAG_NO_CULL) == 0;
 
   bool busy = false;
   bool coop = false;  // RT_TRACE_COOP: four lanes per ray (wave-uniform)
@@ -1151,7 +1193,7 @@ void wf_trace(const WFParams W) {
     // refill once RT_REFILL_MIN lanes are idle (or the whole wave): the refill code runs for the
     // idle lanes only, so doing it every iteration for one or two lanes costs more issue slots
     // than the lanes it brings back
-    if (idle && !drained && (__popcll(idle) >= (STATIC ? RT_REFILL_MIN_SMALL : RT_REFILL_MIN) || idle == __ballot(true))) {
+    if (idle && !drained && (__popcll(idle) >= (STATIC ? RT_REFILL_MIN_SMALL : AHK ? RT_REFILL_MIN_AH : RT_REFILL_MIN) || idle == __ballot(true))) {
       if (pool_next >= pool_end) {
         while (true) {  // (wave-uniform)
           // (small passes: the segments split what the static shares leave, claimed in 64s)
@@ -1162,7 +1204,7 @@ void wf_trace(const WFParams W) {
           const unsigned int chunk = STATIC ? RT_TAIL_CHUNK
               : min((unsigned)P.pool_chunk, max(RT_TAIL_CHUNK, (left / (seg_waves * RT_GUIDED)) & ~63u));
           unsigned int b = 0;
-          if (lane == 0) b = atomicAdd(&S.cnt[xcnt(seg)], chunk);
+          if (lane == 0) b = atomicAdd(&S.cnt[AHK ? xcnts(seg) : xcnt(seg)], chunk);
           b = lo + __builtin_amdgcn_readfirstlane(__shfl(b, 0));
           if (b < hi) {
             pool_next = b;
@@ -1195,9 +1237,9 @@ void wf_trace(const WFParams W) {
             L.ox = P.pos[0]; L.oy = P.pos[1]; L.oz = P.pos[2];
             L.dx = d.x; L.dy = d.y; L.dz = d.z;
           } else {
-            entry = S.queue[qin][qi];
+            entry = Q[qi];
             const int path = entry >> 1;
-            L.anyhit = (entry & 1) != 0;
+            L.anyhit = KIND == 2 ? true : KIND == 1 ? false : (entry & 1) != 0;
             const float4 oa = L.anyhit ? S.sa[path] : S.ra[path];
             if (P1) {  // 16-B rays from pass 0
               p1_ray(S, (unsigned)W.n_frames, (unsigned)path, oa, L.ox, L.oy, L.oz);
@@ -1237,7 +1279,7 @@ void wf_trace(const WFParams W) {
     } else if (busy) {
       if (L.tri_i < L.tri_end) {
         if (COUNT) { v_tri++; ray_steps++; }
-        if (tl_triangle<WIDE>(P, L, L.tri_i++) && L.anyhit) {
+        if (tl_triangle<WIDE, AHK>(P, L, L.tri_i++) && (AHK || (KIND == 0 && L.anyhit))) {
           finished = true;
           L.tri_end = L.tri_i;
         }
@@ -1260,7 +1302,7 @@ void wf_trace(const WFParams W) {
             }
           }
           const int sp0 = L.sp;
-          if (WIDE) needPop = tl_qnode<false>(P, L, TS, cull);
+          if (WIDE) needPop = tl_qnode<false, !AHK || RT_SHADOW_SORT>(P, L, TS, cull);
           else tl_node(P, L, TS, cull);
           if (COUNT) v_ovf += (unsigned)max(0, L.sp - max(sp0, TS.KL));  // entries pushed to the overflow column
         }
@@ -1818,7 +1860,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   __shared__ int la[256 * SH_SUB];
   __shared__ int lsort[256 * SH_SUB];  // the block's paths, grouped by shade_key
   __shared__ unsigned int lhist[SH_KEYS], lofs[SH_KEYS];
-  __shared__ unsigned int lc[5];  // queue count (shadow rays), active count, queue base, active base, continuations
+  __shared__ unsigned int lc[6];  // queue count (shadow rays), active count, queue base, active base, continuations, (split) their base
   constexpr unsigned int kRecs = 256u * SH_SUB / 64u + 1u;  // pixels a block-iteration spans at >= 64 frames
   __shared__ float4 lrec[CAM ? kCamRec * kRecs : 1];
   // 4 waves/SIMD = 4 blocks per CU: the block's LDS must fit a quarter of the CU's 160 KB
@@ -1831,7 +1873,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   const unsigned int nfr = (unsigned int)W.n_frames;
   constexpr bool camrec = CAM;
   const unsigned int na = CAM || W.cam_n ? W.cam_n : S.cnt[ca(in)];
-  const unsigned int nq_in = CAM || W.cam_n ? W.cam_n : S.cnt[cq(in)];
+  const unsigned int nq_in = CAM || W.cam_n ? W.cam_n : S.cnt[cq(in)] + (W.split ? S.cnt[cqs(in)] : 0u);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.cnt[kCntFetch] = 0u;  // fetch counter of the next trace pass
     if (na) {
@@ -1839,7 +1881,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
       if (W.pass <= 1) atomicAdd(&P.stats[18 + W.pass], (unsigned long long)na);  // pass0_steps, pass1_steps
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < 8u) S.cnt[xcnt(threadIdx.x)] = 0u;  // (the next trace pass's segment counters)
+  if (blockIdx.x == 0 && threadIdx.x < 16u)  // (the next trace pass's segment counters, both queues)
+    S.cnt[threadIdx.x < 8u ? xcnt(threadIdx.x) : xcnts(threadIdx.x - 8u)] = 0u;
   const Env E{P.hdr, P.cache, P.light, P.hdr_w, P.hdr_h, P.hdr_res, P.env_angle, P.env_intensity};
   unsigned long long nrays = 0, nsamples = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1915,12 +1958,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[cq(out)], lc[0] + lc[4]) : 0u;
+    if (W.split) {  // shadow rays and continuations to their own queues
+      lc[2] = lc[0] ? atomicAdd(&S.cnt[cqs(out)], lc[0]) : 0u;
+      lc[5] = lc[4] ? atomicAdd(&S.cnt[cq(out)], lc[4]) : 0u;
+    } else {
+      lc[2] = (lc[0] + lc[4]) ? atomicAdd(&S.cnt[cq(out)], lc[0] + lc[4]) : 0u;
+    }
     lc[3] = lc[1] ? atomicAdd(&S.cnt[ca(out)], lc[1]) : 0u;
   }
   __syncthreads();
-  for (unsigned int j = threadIdx.x; j < lc[0] + lc[4]; j += 256u)
-    S.queue[out][lc[2] + j] = j < lc[0] ? lq[j] : lq[2 * 256 * SH_SUB - 1 - (j - lc[0])];
+  if (W.split) {
+    for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue_s[out][lc[2] + j] = lq[j];
+    for (unsigned int j = threadIdx.x; j < lc[4]; j += 256u) S.queue[out][lc[5] + j] = lq[2 * 256 * SH_SUB - 1 - j];
+  } else {
+    for (unsigned int j = threadIdx.x; j < lc[0] + lc[4]; j += 256u)
+      S.queue[out][lc[2] + j] = j < lc[0] ? lq[j] : lq[2 * 256 * SH_SUB - 1 - (j - lc[0])];
+  }
   for (unsigned int j = threadIdx.x; j < lc[1]; j += 256u) S.active[out][lc[3] + j] = la[j];
   __syncthreads();
   }
