@@ -23,6 +23,9 @@
 #ifndef RT_SPLIT_KINDS  // bulk groups trace shadow rays and continuations in launches of their own (round 6)
 #define RT_SPLIT_KINDS 1
 #endif
+#ifndef RT_SPLIT_CONT_FIRST  // split queues: the continuations' launch first (1) or the shadow rays' (0)
+#define RT_SPLIT_CONT_FIRST 0  // C3 1 vs 0: -0.16% (profiles/r06_ab_split_knobs_C3.log)
+#endif
 #include "tri_filter.h"
 
 using rtd::GNode;
@@ -697,12 +700,12 @@ void launch_trace_w(rt_ctx* c, dim3 grid, const rtd::WFParams& WP, hipStream_t s
     return;
   }
   if (WP.split && !WP.cam_n && !COUNT && WIDE) {  // split queues: the shadow rays, then the continuations
-    if (p1) {
-      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 2>), grid, dim3(256), c->trace_lds, st, WP);
-      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 1>), grid, dim3(256), c->trace_lds, st, WP);
-    } else {
-      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 2>), grid, dim3(256), c->trace_lds, st, WP);
-      hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 1>), grid, dim3(256), c->trace_lds, st, WP);
+    for (int k = 0; k < 2; k++) {
+      const bool shadow = (k == 0) != (RT_SPLIT_CONT_FIRST != 0);
+      if (p1 && shadow) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 2>), grid, dim3(256), c->trace_lds, st, WP);
+      else if (p1) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, true, 1>), grid, dim3(256), c->trace_lds, st, WP);
+      else if (shadow) hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 2>), grid, dim3(256), c->trace_lds, st, WP);
+      else hipLaunchKernelGGL((rtd::wf_trace<false, true, false, false, false, 1>), grid, dim3(256), c->trace_lds, st, WP);
     }
     return;
   }

@@ -1050,8 +1050,10 @@ RTD int coop_move(TraceLane& L, const TraceStack& TS, unsigned long long live, i
                    // profiles/r06_rank_ab_claim_knobs_C3.log)
 #define RT_GUIDED 3u
 #endif
-#ifndef RT_REFILL_MIN_AH  // the any-hit kernel's refill threshold (split queues)
-#define RT_REFILL_MIN_AH RT_REFILL_MIN
+#ifndef RT_REFILL_MIN_AH  // the any-hit kernel's refill threshold (split queues): C3 12 / 20 / 28 -0.55 / 0 / +0.44%
+                          // (profiles/r06_ab_split_knobs_C3.log), 28 / 36 / 44 0 / -0.17 / -0.45%, with the
+                          // closest-hit kernel's 16 / 24 -0.45 / -0.05% (profiles/r06_ab_split_refill_C3.log)
+#define RT_REFILL_MIN_AH 28
 #endif
 #ifndef RT_REFILL_MIN_SMALL  // the small passes' refill threshold: C3 1080p one-frame calls 4 / 6 / 8 / 12 / 16 vs 20:
                              // -0.5 / -0.7 / -1.1, -0.6 / -0.9, -0.5 / -0.7% back-to-back (round 5,
