@@ -57,6 +57,7 @@ struct KParams {
   const float4* __restrict__ trx;   // traversal record, 3 per triangle: {p1, Ng.x} {R2, Ng.y} {R3, Ng.z}
   float tri_k1, tri_k0;             // its edge-filter margin (csrc/common/tri_filter.h)
   const float4* __restrict__ trin;  // 3 per triangle: {n1, matid bits} {n2, leaf rank bits} {n3, 0}
+  const float4* __restrict__ hrec;  // 8 per triangle (one 128-B line): tri's 3 then trin's 3, 2 unused
   const float4* __restrict__ mats;  // 8 per material
   const float4* __restrict__ hdr;
   const float2* __restrict__ cache;  // hdrCache.rg (hdr.w holds hdrCache.b)
@@ -461,10 +462,14 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, float* _
 }
 
 // rt_update_materials: the material id lives in .w of each triangle's first normal texel
-__global__ __launch_bounds__(256) void rt_set_material_kernel(float4* __restrict__ trin, int first, int count,
-                                                             int id) {
+// (and of the shade's hit record, KParams::hrec)
+__global__ __launch_bounds__(256) void rt_set_material_kernel(float4* __restrict__ trin, float4* __restrict__ hrec,
+                                                             int first, int count, int id) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) trin[3 * (size_t)(first + i)].w = __int_as_float(id);
+  if (i < count) {
+    trin[3 * (size_t)(first + i)].w = __int_as_float(id);
+    hrec[8 * (size_t)(first + i) + 3].w = __int_as_float(id);
+  }
 }
 
 // ------------------------------------------------------------ display (rt_tonemap)

@@ -23,6 +23,10 @@
 #ifndef RT_SPLIT_KINDS  // bulk groups trace shadow rays and continuations in launches of their own (round 6)
 #define RT_SPLIT_KINDS 1
 #endif
+#ifndef RT_SPLIT_PASSES  // the last pass traced split (later ones: one launch, both kinds); C3 3 / 4 / 5 / 6 / 7 vs 8:
+                         // -0.18, -0.15 / +0.19, +0.22 / -0.03 / -0.04% (profiles/r06_ab_split_passes_C3.log)
+#define RT_SPLIT_PASSES 5
+#endif
 #ifndef RT_SPLIT_CONT_FIRST  // split queues: the continuations' launch first (1) or the shadow rays' (0)
 #define RT_SPLIT_CONT_FIRST 0  // C3 1 vs 0: -0.16% (profiles/r06_ab_split_knobs_C3.log)
 #endif
@@ -47,6 +51,7 @@ struct rt_ctx {
   double tri_k1 = 0.0, tri_k0 = 0.0;  // their edge-filter margin
   int tri_flagged = 0;
   float4* d_trin = nullptr;
+  float4* d_hrec = nullptr;  // the shade's hit records (KParams::hrec)
   float4* d_mats = nullptr;
   int n_tri = 0, n_mats = 0, root = 0, has_scene = 0, stack_entries = 2;
   double cull_R = 0.0, cull_K = 0.0, cull_off = 0.0;  // culling bound of the scene (cull_bound_stats)
@@ -108,6 +113,7 @@ struct rt_ctx {
   int trace_bpc = 0, trace_bpc0 = 0;          // wavefront traversal blocks/CU (passes >= 1, pass 0)
   int trace_lds_entries = 0, trace_lds = 0;
   int split_kinds = RT_SPLIT_KINDS;  // bulk groups: shadow rays and continuations in queues of their own
+  int split_passes = RT_SPLIT_PASSES;  // ... in passes 1 .. split_passes (later ones: one queue, one launch)
   // per-frame loopNum / randOrigin of one render call: pinned host staging -> device table;
   // ft[0] for batched calls, ft[1 + p] for pipelined one-frame calls on pipeline set p
   struct FrameTable {
@@ -609,6 +615,7 @@ int occupancy(rt_ctx* c) {
   int kl = 8;  // 16 KiB per block: LDS leaves room for 8 waves/SIMD (12 entries: 6; C3 5853 -> 5959 at 10, 6155 at 8 with the dual schedule at 8 waves)
   if (const char* e = knob("RT_LDS_STACK")) kl = atoi(e);
   if (const char* e = knob("RT_SPLIT_KINDS")) c->split_kinds = atoi(e);
+  if (const char* e = knob("RT_SPLIT_PASSES")) c->split_passes = atoi(e);
   kl = std::max(1, std::min(kl, std::max(c->stack_entries, c->qstack_entries)));
   c->trace_lds_entries = kl;
   c->trace_lds = kl * 256 * 8;
@@ -911,7 +918,7 @@ int rt_destroy(rt_ctx* c) {
   for (auto& e : c->set_free) if (e) (void)hipEventDestroy(e);
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   if (c->busy_anchor) (void)hipEventDestroy(c->busy_anchor);
-  dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trx); dfree(c->d_trin); dfree(c->d_mats);
+  dfree(c->d_nodes); dfree(c->d_qnodes); dfree(c->d_tri); dfree(c->d_trx); dfree(c->d_trin); dfree(c->d_hrec); dfree(c->d_mats);
   for (auto& t : c->light) {
     dfree(t.d);
     if (t.last_use) (void)hipEventDestroy(t.last_use);
@@ -1066,6 +1073,15 @@ int rt_set_scene(rt_ctx* c, const rt_scene_soa* s) {
     c->tri_k1 = k.k1; c->tri_k0 = k.k0; c->tri_flagged = k.flagged;
   }
   if ((rc = upload(c, (void**)&c->d_trin, trin.data(), trin.size() * sizeof(float4)))) return rc;
+  {  // hit records: tri's three texels then trin's, one 128-B line per triangle
+    std::vector<float4> hr(8 * std::max<size_t>(1, (size_t)nt), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (size_t i = 0; i < (size_t)nt; i++)
+      for (int k = 0; k < 3; k++) {
+        hr[8 * i + k] = tri[3 * i + k];
+        hr[8 * i + 3 + k] = trin[3 * i + k];
+      }
+    if ((rc = upload(c, (void**)&c->d_hrec, hr.data(), hr.size() * sizeof(float4)))) return rc;
+  }
   if ((rc = upload(c, (void**)&c->d_mats, mt.data(), mt.size() * sizeof(float)))) return rc;
   c->n_tri = nt;
   c->n_mats = s->n_materials;
@@ -1146,7 +1162,7 @@ int rt_update_materials(rt_ctx* c, int32_t first, int32_t count, const rt_materi
   for (int i = first; i < first + count; i++) c->tri_mat[i] = id;
   if (count > 0) {
     hipLaunchKernelGGL(rtd::rt_set_material_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream,
-                       c->d_trin, first, count, id);
+                       c->d_trin, c->d_hrec, first, count, id);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1522,7 +1538,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       const double sc = es ? atof(es) : 1.0;
       P.cull_eps = (eps * sc < 1e30) ? (float)(eps * sc) : INFINITY;
     }
-    P.tri = c->d_tri; P.trin = c->d_trin; P.mats = c->d_mats;
+    P.tri = c->d_tri; P.trin = c->d_trin; P.hrec = c->d_hrec; P.mats = c->d_mats;
     {  // edge-filter margin, rounded up (x (1 + 2^-20)); RT_TRI_MARGIN_SCALE (tests only): 0 makes
        // the filter decide every point, the negative control of tests/test_gpu_tri_filter.py
       const char* ms = knob("RT_TRI_MARGIN_SCALE");
@@ -1575,6 +1591,7 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
       rtd::WFParams WG[rt_ctx::MAX_GROUPS];
       hipStream_t sg[rt_ctx::MAX_GROUPS];
       unsigned int slots_g[rt_ctx::MAX_GROUPS];
+      int split_g[rt_ctx::MAX_GROUPS] = {};
       // pixel ranges of the groups: even, or after rt_order_work the costly head as group 0 and
       // the rest split evenly (dev: RT_GROUP_SPLIT = group 0's share)
       size_t b0 = std::min(c->order_head, (size_t)c->n_valid);
@@ -1629,7 +1646,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.fuse_blend = (!pipe && WP.n_frames == 1 && (pix_split || G == 1) && !count) ? 1 : 0;
         slots_g[g] = (unsigned)(f1 - f0) * (w1 - w0);
         // bulk groups (the wf_shade<..., SH_SUB_BULK / CAM> launches) queue the two ray kinds apart
-        WP.split = (c->split_kinds && c->wide && !count && !c->tile_cost_on && slots_g[g] > c->finish_slots && !WP.fuse_blend) ? 1 : 0;
+        // (per pass below: passes 1 .. split_passes)
+        split_g[g] = (c->split_kinds && c->wide && !count && !c->tile_cost_on && slots_g[g] > c->finish_slots && !WP.fuse_blend) ? 1 : 0;
         sg[g] = pipe ? ps : g == 0 ? c->stream : c->aux[g];
       }
       // camera directions of this call's pixels (every group reads them)
@@ -1674,6 +1692,8 @@ int rt_render_async(rt_ctx* c, const rt_frame_params* fp, const float* rand_orig
         WP.p1_compact = (finish && fin_pass <= 1) ? 0 : 1;
         for (int pass = 0; pass <= last_pass; pass++) {
           WP.pass = pass;
+          WP.split = (split_g[g] && pass >= 1 && pass <= c->split_passes) ? 1 : 0;
+          WP.split_out = (split_g[g] && pass + 1 <= c->split_passes) ? 1 : 0;
           if (finish && pass == fin_pass) {
             const dim3 fgrid((unsigned)(c->n_cus * (pipe ? c->pipe_finish_bpc : c->finish_bpc)));
 #ifdef RT_DEV

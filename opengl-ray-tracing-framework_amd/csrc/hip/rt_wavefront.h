@@ -149,8 +149,9 @@ struct WFParams {
   // RT:1552) instead of writing fin for a wf_blend launch after the last pass
   int fuse_blend;
   // bulk groups: the shade queues shadow rays (queue_s, cqs) and continuations (queue, cq) apart,
-  // and each secondary pass traces them in two launches, wf_trace<..., KIND = 2> and <..., 1>
-  int split;
+  // and each secondary pass traces them in two launches, wf_trace<..., KIND = 2> and <..., 1>.
+  // split: this pass's rays are in split queues; split_out: the shade queues the next pass's apart
+  int split, split_out;
 };
 
 // Map a work index of this rank to (pixel, accumulation index); false outside the frame.
@@ -1430,9 +1431,18 @@ struct HitGeom {
   f3 Pp, Ns;
   int nmat;
 };
+// The six texels come from the triangle's 128-B hit record (KParams::hrec: one cache line) rather
+// than from tri and trin, whose 48-B records straddle a line boundary 37% of the time (2.7 lines
+// per hit instead of 1, fetched from MALL: the continuation's triangle is a scattered access)
+#ifndef RT_HREC
+#define RT_HREC 1
+#endif
 RTD HitGeom hit_geom(const KParams& P, int tri, f3 ro, f3 rd) {
-  const float4 A = P.tri[3 * tri], B = P.tri[3 * tri + 1], Cc = P.tri[3 * tri + 2];
-  const float4 N1 = P.trin[3 * tri], N2 = P.trin[3 * tri + 1], N3 = P.trin[3 * tri + 2];
+  const float4* h4 = RT_HREC ? P.hrec + 8 * tri : nullptr;
+  const float4 A = RT_HREC ? h4[0] : P.tri[3 * tri], B = RT_HREC ? h4[1] : P.tri[3 * tri + 1],
+               Cc = RT_HREC ? h4[2] : P.tri[3 * tri + 2];
+  const float4 N1 = RT_HREC ? h4[3] : P.trin[3 * tri], N2 = RT_HREC ? h4[4] : P.trin[3 * tri + 1],
+               N3 = RT_HREC ? h4[5] : P.trin[3 * tri + 2];
   const f3 p1 = xyz(A), p2 = xyz(B), p3 = xyz(Cc);
   const f3 ng = mk3(A.w, B.w, Cc.w);
   HitGeom h;
@@ -1960,7 +1970,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (W.split) {  // shadow rays and continuations to their own queues
+    if (W.split_out) {  // shadow rays and continuations to their own queues
       lc[2] = lc[0] ? atomicAdd(&S.cnt[cqs(out)], lc[0]) : 0u;
       lc[5] = lc[4] ? atomicAdd(&S.cnt[cq(out)], lc[4]) : 0u;
     } else {
@@ -1969,7 +1979,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADE_WP
     lc[3] = lc[1] ? atomicAdd(&S.cnt[ca(out)], lc[1]) : 0u;
   }
   __syncthreads();
-  if (W.split) {
+  if (W.split_out) {
     for (unsigned int j = threadIdx.x; j < lc[0]; j += 256u) S.queue_s[out][lc[2] + j] = lq[j];
     for (unsigned int j = threadIdx.x; j < lc[4]; j += 256u) S.queue[out][lc[5] + j] = lq[2 * 256 * SH_SUB - 1 - j];
   } else {

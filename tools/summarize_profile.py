@@ -19,9 +19,14 @@ wf_trace<true, ...> (the COUNT instantiation that frame runs) on is dropped, wf_
 (its 18 near-empty launches had been averaged in).  probe_avg_launch_ms = the mean of the
 last `probe_trace_launches` wf_trace launches before that frame in the trace pass: bench.py's
 standalone probe (one frame group, RT_FLAG_SERIAL), the figure its roofline divides by.
+A wf_trace "launch" is one bounce pass's traversal: with split queues (round 6) a secondary pass is
+two dispatches, wf_trace<..., 2> (its shadow rays) then wf_trace<..., 1> (its continuations), so
+wf_trace's durations and counters are summed over a pass's dispatches (an any-hit dispatch joins
+the dispatch after it) and `dispatches` breaks the trace pass down per instantiation.
 """
 import csv
 import json
+import re
 import shutil
 import statistics
 import sys
@@ -50,12 +55,40 @@ def rows(path):
     return [r for r in rs if cut is None or int(r["Dispatch_Id"]) < cut]
 
 
+def any_hit(full):
+    """a wf_trace<..., 2> dispatch: the shadow-ray half of a split pass (joins the next dispatch)"""
+    return re.search(r"wf_trace<[^>]*, 2>", full) is not None
+
+
+def launch_key(k, r, state):
+    """the launch a dispatch belongs to: its own Dispatch_Id, or for an any-hit wf_trace dispatch
+    the next wf_trace dispatch's (state carries the pending ones)"""
+    d = r["Dispatch_Id"]
+    if k != "wf_trace":
+        return d
+    if any_hit(r["Kernel_Name"]):
+        state.setdefault("pend", []).append(d)
+        return None
+    for p in state.pop("pend", []):
+        state.setdefault("alias", {})[p] = d
+    return d
+
+
 shutil.copyfile(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
 durs, regs = defaultdict(list), {}
+inst = defaultdict(list)  # wf_trace instantiation -> dispatch durations (trace pass)
+carry = 0.0
 for r in rows(src / "trace" / "run_kernel_trace.csv"):
     k = kname(r["Kernel_Name"])
     if k:
-        durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        ms_ = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        if k == "wf_trace":
+            inst[r["Kernel_Name"].split("(")[0].replace("void rtd::", "")].append(ms_)
+            if any_hit(r["Kernel_Name"]):
+                carry += ms_
+                continue
+            ms_, carry = ms_ + carry, 0.0
+        durs[k].append(ms_)
         regs[k] = {"vgpr": int(r.get("Arch_VGPR_Count", r.get("VGPR_Count", 0)) or 0),
                    "sgpr": int(r.get("SGPR_Count", 0) or 0), "lds": int(r.get("LDS_Block_Size", 0) or 0),
                    "scratch": int(r.get("Scratch_Size", 0) or 0)}
@@ -66,24 +99,40 @@ def standalone(name):
     p = src / name / "run_kernel_trace.csv"
     out = defaultdict(dict)
     if p.exists():
+        st, carry = {}, 0.0
         for r in rows(p):
             k = kname(r["Kernel_Name"])
             if k:
-                out[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                ms_ = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                if launch_key(k, r, st) is None:
+                    carry += ms_
+                    continue
+                out[k][r["Dispatch_Id"]] = ms_ + (carry if k == "wf_trace" else 0.0)
+                if k == "wf_trace":
+                    carry = 0.0
     return out
 
 
 def counters(name):
     """per kernel: counter -> mean over launches (and the durations seen in that pass)"""
-    out = defaultdict(lambda: defaultdict(list))
+    out = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> launch -> value
     p = src / name / "run_counter_collection.csv"
     if not p.exists():
         return {}
-    for r in rows(p):
+    st = {}
+    rs = rows(p)
+    for r in rs:  # (a dispatch's counters come in several rows: resolve launches in dispatch order first)
+        k = kname(r["Kernel_Name"])
+        if k and r["Dispatch_Id"] not in st.setdefault("seen", set()):
+            st["seen"].add(r["Dispatch_Id"])
+            launch_key(k, r, st)
+    alias = st.get("alias", {})
+    for r in rs:
         k = kname(r["Kernel_Name"])
         if k:
-            out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: statistics.mean(v) for c, v in d.items()} for k, d in out.items()}
+            d = alias.get(r["Dispatch_Id"], r["Dispatch_Id"])
+            out[k][r["Counter_Name"]][d] += float(r["Counter_Value"])
+    return {k: {c: statistics.mean(v.values()) for c, v in d.items()} for k, d in out.items()}
 
 
 PASSES = ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_tcc")
@@ -122,6 +171,9 @@ for k in KERNELS:
     if k == "wf_trace" and npr and len(durs[k]) > npr:
         e["probe_avg_launch_ms"] = round(statistics.mean(durs[k][-npr:]), 4)
         e["probe_launches"] = npr
+    if k == "wf_trace" and inst:
+        e["dispatches"] = {n: {"count": len(v), "avg_ms": round(statistics.mean(v), 4), "total_ms": round(sum(v), 2)}
+                           for n, v in inst.items()}
     if c.get("TCC_HIT_sum"):
         e["l2_hit"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
     summary["kernels"][k] = e
