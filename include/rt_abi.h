@@ -48,8 +48,10 @@
  *    unchanged, so that call with the ABI-4 size fills them (tests/c/abi_stats.c).
  *    RT_FLAG_SORTED_TRAVERSAL is accepted and has no effect (the octant-ordered traversal it
  *    switched off was removed).
+ * 6: rt_gather moves the tiles with RCCL when the contexts sit on distinct devices;
+ *    rt_gather_ex chooses the transport, rt_gather_last_transport reports it.  Nothing else changed.
  * A binding checks rt_abi_version() at load time. */
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 #ifdef __cplusplus
 extern "C" {
@@ -243,12 +245,21 @@ int rt_copy_accum_device(rt_ctx* ctx, void* dst_device, size_t bytes);
 int rt_assemble_frame(rt_ctx* ctx, const void* gathered_device, int32_t world, void* frame_device);
 /* Single-process form of the frame-end gather (SURVEY §8(b) rt_gather, §8(e)): ctxs[r] renders
  * rank r of a world of n (rt_resize tiling; one context per device, or several on one).  After
- * the work queued on each context, its accumulation tiles are copied peer to peer (xGMI between
- * GPUs) into ctxs[0]'s device, un-permuted there (rt_assemble_frame) and read back: full_rgb =
- * width*height*3 floats, row 0 = bottom (RT_LAYOUT_FRAME).  Synchronous; errors land in
- * rt_last_error(ctxs[0]).  One process per GPU uses rt_copy_accum_device + an RCCL gather +
- * rt_assemble_frame instead (bench.py). */
+ * the work queued on each context, its accumulation tiles reach ctxs[0]'s device, are un-permuted
+ * there (rt_assemble_frame) and read back: full_rgb = width*height*3 floats, row 0 = bottom
+ * (RT_LAYOUT_FRAME).  Transport: with one device per context an RCCL gather over xGMI
+ * (ncclCommInitAll over the contexts' devices, kept in ctxs[0]; ncclSend from every rank's stream,
+ * ncclRecv on rank 0's, in one group), else peer copies (several contexts on one device).
+ * Synchronous; errors land in rt_last_error(ctxs[0]).  One process per GPU uses
+ * rt_copy_accum_device + a torch.distributed (RCCL) gather + rt_assemble_frame instead (bench.py). */
 int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb);
+enum { RT_GATHER_AUTO = 0, RT_GATHER_RCCL = 1, RT_GATHER_PEER = 2 };
+/* rt_gather with the transport chosen: RT_GATHER_AUTO (rt_gather's rule), RT_GATHER_RCCL
+ * (RT_ERR_ARG unless every context has its own device), RT_GATHER_PEER (hipMemcpyPeerAsync). */
+int rt_gather_ex(rt_ctx* const* ctxs, int32_t n, float* full_rgb, int32_t transport);
+/* The transport ctx's last rt_gather / rt_gather_ex as ctxs[0] used (RT_GATHER_RCCL or
+ * RT_GATHER_PEER; 0 before any). */
+int rt_gather_last_transport(const rt_ctx* ctx);
 
 /* Display / screenshot — replaces the tone-mapping pass
  * (src/shaders/fragment_shader_tone_mapping.glsl:66-93, main.cpp:215-227) or the screen blit

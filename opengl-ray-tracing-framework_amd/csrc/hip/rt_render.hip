@@ -4,6 +4,7 @@
 // buffers and launches the persistent kernel.  No fallback path: without a HIP device every
 // entry point returns RT_ERR_NODEVICE / RT_ERR_HIP.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -134,6 +135,11 @@ struct rt_ctx {
   void* d_disp = nullptr;                     // rt_tonemap output (W*H*3 bytes)
   size_t disp_bytes = 0;
   void* d_gather = nullptr;                   // rt_gather on rank 0: every rank's tiles, then the frame
+  // rt_gather over RCCL: the communicators (one per rank, this process drives them all) of the
+  // device set ctxs[0] last gathered over, and the transport its last gather used
+  std::vector<int> rccl_devs;
+  std::vector<ncclComm_t> rccl_comms;
+  int gather_transport = 0;
   size_t gather_bytes = 0;
   size_t stack_ovf_bytes = 0;
   // wavefront path state (one slot per local pixel)
@@ -946,6 +952,7 @@ int rt_destroy(rt_ctx* c) {
   dfree(c->d_stack_ovf);
   dfree(c->d_disp);
   dfree(c->d_gather);
+  for (auto& m : c->rccl_comms) (void)ncclCommDestroy(m);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -1921,6 +1928,7 @@ int rt_synchronize(rt_ctx* c) {
 }
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+int rt_gather_last_transport(const rt_ctx* c) { return c ? c->gather_transport : RT_ERR_ARG; }
 
 // rt_stats_get and rt_render write the ABI-3 struct (through p1_rays), the size every binding of
 // that header allocated; the fields added since reach a caller only through rt_stats_get_sized
@@ -2242,7 +2250,51 @@ int rt_assemble_frame(rt_ctx* c, const void* gathered, int32_t world, void* fram
 }
 
 int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb) {
+  return rt_gather_ex(ctxs, n, full_rgb, RT_GATHER_AUTO);
+}
+
+// RCCL form of the gather: one communicator per context's device (ncclCommInitAll,
+// this thread drives every rank), each rank's tiles sent to rank 0 on its own stream after its
+// queued work, rank 0 receiving all of them (its own included) into the rank-major buffer, in one
+// group.  The communicators stay in ctxs[0] for the next gather over the same devices.
+static int gather_rccl(rt_ctx* const* ctxs, int n, char* g, size_t part) {
+  rt_ctx* c0 = ctxs[0];
+  std::vector<int> devs(n);
+  for (int r = 0; r < n; r++) devs[r] = ctxs[r]->device;
+  auto nfail = [&](const char* what, ncclResult_t e) {
+    return fail(c0, RT_ERR_HIP, std::string("rt_gather: ") + what + ": " + ncclGetErrorString(e));
+  };
+  if (c0->rccl_devs != devs) {
+    for (auto& m : c0->rccl_comms) (void)ncclCommDestroy(m);
+    c0->rccl_comms.assign(n, nullptr);
+    c0->rccl_devs.clear();
+    const ncclResult_t e = ncclCommInitAll(c0->rccl_comms.data(), n, devs.data());
+    if (e != ncclSuccess) {
+      c0->rccl_comms.clear();
+      return nfail("ncclCommInitAll", e);
+    }
+    c0->rccl_devs = devs;
+  }
+  const size_t cnt = part / sizeof(float);
+  ncclResult_t e = ncclGroupStart();
+  if (e != ncclSuccess) return nfail("ncclGroupStart", e);
+  for (int r = 0; r < n && e == ncclSuccess; r++) {
+    (void)hipSetDevice(ctxs[r]->device);
+    e = ncclSend(ctxs[r]->d_accum, cnt, ncclFloat32, 0, c0->rccl_comms[r], ctxs[r]->stream);
+  }
+  (void)hipSetDevice(c0->device);
+  for (int r = 0; r < n && e == ncclSuccess; r++)
+    e = ncclRecv(g + (size_t)r * part, cnt, ncclFloat32, r, c0->rccl_comms[0], c0->stream);
+  const ncclResult_t eg = ncclGroupEnd();
+  (void)hipSetDevice(c0->device);
+  if (e != ncclSuccess) return nfail("ncclSend / ncclRecv", e);
+  if (eg != ncclSuccess) return nfail("ncclGroupEnd", eg);
+  return RT_OK;
+}
+
+int rt_gather_ex(rt_ctx* const* ctxs, int32_t n, float* full_rgb, int32_t transport) {
   if (!ctxs || n <= 0 || !full_rgb || !ctxs[0]) return RT_ERR_ARG;
+  if (transport != RT_GATHER_AUTO && transport != RT_GATHER_RCCL && transport != RT_GATHER_PEER) return RT_ERR_ARG;
   rt_ctx* c0 = ctxs[0];
   for (int r = 0; r < n; r++) {
     const rt_ctx* c = ctxs[r];
@@ -2253,6 +2305,12 @@ int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb) {
         c->max_local_tiles != c0->max_local_tiles || c->owner != c0->owner)
       return fail(c0, RT_ERR_ARG, "rt_gather: contexts differ in frame size or tiling");
   }
+  bool distinct = true;  // one device per context: what an RCCL communicator needs
+  for (int r = 0; r < n; r++)
+    for (int q = 0; q < r; q++) distinct &= ctxs[r]->device != ctxs[q]->device;
+  if (transport == RT_GATHER_AUTO) transport = distinct ? RT_GATHER_RCCL : RT_GATHER_PEER;
+  if (transport == RT_GATHER_RCCL && !distinct)
+    return fail(c0, RT_ERR_ARG, "rt_gather: RCCL needs one device per context (use RT_GATHER_PEER)");
   const size_t part = (size_t)std::max(1, c0->max_local_tiles) * c0->tile_w * c0->tile_h * sizeof(float4);
   const size_t frame = (size_t)c0->W * c0->H * 3 * sizeof(float);
   HIPCHK(c0, hipSetDevice(c0->device));
@@ -2269,7 +2327,9 @@ int rt_gather(rt_ctx* const* ctxs, int32_t n, float* full_rgb) {
     (void)hipSetDevice(c0->device);
   };
   int rc = RT_OK;
-  for (int r = 0; r < n && rc == RT_OK; r++) {
+  c0->gather_transport = transport;
+  if (transport == RT_GATHER_RCCL) rc = gather_rccl(ctxs, n, g, part);
+  for (int r = 0; r < n && rc == RT_OK && transport == RT_GATHER_PEER; r++) {
     const rt_ctx* c = ctxs[r];
     hipEvent_t e = nullptr;
     hipError_t he = hipSetDevice(c->device);

@@ -26,7 +26,8 @@ RT_FLAG_NO_FINISH = 8
 RT_FLAG_FINISH = 16
 RT_FLAG_SERIAL = 32
 RT_FLAG_SORTED_TRAVERSAL = 64
-RT_ABI_VERSION = 5
+RT_ABI_VERSION = 6
+RT_GATHER_AUTO, RT_GATHER_RCCL, RT_GATHER_PEER = 0, 1, 2
 RT_LAYOUT_FRAME, RT_LAYOUT_LOCAL_TILES = 0, 1
 
 _f32p = C.POINTER(C.c_float)
@@ -40,7 +41,8 @@ ABI_SYMBOLS = (
     "rt_get_stream", "rt_set_stream", "rt_read_accum", "rt_write_accum", "rt_accum_device", "rt_copy_accum_device",
     "rt_assemble_frame", "rt_tonemap", "rt_set_max_paths", "rt_gather", "rt_set_tile_owners", "rt_get_tile_owners",
     "rt_tile_costs", "rt_set_finish", "rt_order_work", "rt_set_pipeline",
-    "rt_tonemap_async", "rt_display_fetch", "rt_stats_get_sized", "rt_abi_version",
+    "rt_tonemap_async", "rt_display_fetch", "rt_stats_get_sized", "rt_abi_version", "rt_gather_ex",
+    "rt_gather_last_transport",
 )
 RT_DISPLAY_TONEMAP, RT_DISPLAY_GAMMA = 1, 2
 
@@ -208,6 +210,9 @@ def _bind(L: C.CDLL) -> C.CDLL:
     L.rt_get_tile_owners.argtypes = [vp, _i32p, C.c_int32]
     L.rt_tile_costs.argtypes = [vp, C.POINTER(RtFrameParams), _f32p, C.c_int32, C.POINTER(C.c_uint64)]
     L.rt_gather.argtypes = [C.POINTER(vp), C.c_int32, _f32p]
+    if hasattr(L, "rt_gather_ex"):
+        L.rt_gather_ex.argtypes = [C.POINTER(vp), C.c_int32, _f32p, C.c_int32]
+        L.rt_gather_last_transport.argtypes = [vp]
     return L
 
 
@@ -423,14 +428,22 @@ class Renderer:
                     "rt_assemble_frame")
 
     @staticmethod
-    def gather(ranks: Sequence["Renderer"]) -> np.ndarray:
+    def gather(ranks: Sequence["Renderer"], transport: Optional[int] = None) -> np.ndarray:
         """rt_gather: the full (H, W, 3) frame (row 0 = bottom) from contexts ranks[r] = rank r of
-        len(ranks), assembled on ranks[0]'s device (single-process multi-GPU)."""
+        len(ranks), assembled on ranks[0]'s device (single-process multi-GPU); RCCL
+        when every context has its own device, else peer copies (transport: rt_gather_ex's choice)."""
         r0 = ranks[0]
         hs = (C.c_void_p * len(ranks))(*[r._h.value for r in ranks])
         out = np.zeros((r0.height, r0.width, 3), np.float32)
-        r0._check(r0._L.rt_gather(hs, len(ranks), _fp(out)), "rt_gather")
+        if transport is None:
+            r0._check(r0._L.rt_gather(hs, len(ranks), _fp(out)), "rt_gather")
+        else:
+            r0._check(r0._L.rt_gather_ex(hs, len(ranks), _fp(out), int(transport)), "rt_gather_ex")
         return out
+
+    def gather_transport(self) -> int:
+        """the transport of this context's last gather as rank 0 (RT_GATHER_RCCL / RT_GATHER_PEER)"""
+        return int(self._L.rt_gather_last_transport(self._h))
 
     def tonemap(self, flags: int = RT_DISPLAY_TONEMAP | RT_DISPLAY_GAMMA, frame_ptr: Optional[int] = None) -> np.ndarray:
         """The displayed 8-bit image (H, W, 3), row 0 = top: the tone-mapping pass / screen blit +

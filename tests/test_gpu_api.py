@@ -9,6 +9,7 @@ from helpers import bit_mismatch, frames_for, gpu_render, oracle_render
 from rtamd import configs as cf
 from rtamd import scene_lib as sl
 from rtamd import tiling
+from rtamd.renderer import RT_GATHER_PEER, RT_GATHER_RCCL
 
 pytestmark = pytest.mark.gpu
 
@@ -184,12 +185,49 @@ def test_single_process_gather(gpu_renderer, env_maps):
             r.clear_accum()
             r.render_async(fp, ro)  # no synchronisation: rt_gather orders the copies itself
         img = Renderer.gather(ctxs)
+        assert ctxs[0].gather_transport() == RT_GATHER_PEER  # (contexts sharing a device)
         with pytest.raises(RuntimeError, match="rank r"):
             Renderer.gather([ctxs[1], ctxs[0], ctxs[2]])
+        with pytest.raises(RuntimeError, match="one device per context"):
+            Renderer.gather(ctxs, transport=RT_GATHER_RCCL)
     finally:
         for r in ctxs[1:]:
             r.close()
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+def test_single_process_gather_rccl(gpu_renderer, env_maps):
+    """rt_gather over RCCL: one context per device (every visible device, up to
+    8), each rendering its rank's tiles; the communicators come from ncclCommInitAll, every rank
+    sends its tiles to rank 0 in one group.  On a one-GPU box that is a world of one (rank 0 sends
+    to itself); the frame equals the oracle bit for bit and a second gather reuses the
+    communicators."""
+    import torch
+    from rtamd.renderer import Renderer
+    sd = cf.config_scene("C2")
+    world = max(1, min(8, torch.cuda.device_count()))
+    W, H, T = 72, 40, 16
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, 2)
+    ref, _ = oracle_render(sd, env_maps, W, H, frames)
+    ctxs = [gpu_renderer] + [Renderer(d) for d in range(1, world)]
+    try:
+        for rank, r in enumerate(ctxs):
+            r.set_scene_soa(sd.soa, sd.nodes)
+            r.set_env(env_maps[0], env_maps[1])
+            r.resize(W, H, tile=T, rank=rank, world=world)
+            r.set_loop_num(0)
+            r.clear_accum()
+            r.render_async(fp, ro)
+        img = Renderer.gather(ctxs)
+        assert ctxs[0].gather_transport() == RT_GATHER_RCCL
+        img2 = Renderer.gather(ctxs, transport=RT_GATHER_RCCL)
+        peer = Renderer.gather(ctxs, transport=RT_GATHER_PEER)
+    finally:
+        for r in ctxs[1:]:
+            r.close()
+    assert bit_mismatch(img, ref)[0] == 0.0
+    assert np.array_equal(img, img2) and np.array_equal(img, peer)
 
 
 def test_path_budget_beyond_device_memory_falls_back(env_maps):
