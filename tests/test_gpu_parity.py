@@ -411,3 +411,38 @@ def test_camera_hit_records_match_oracle(gpu_renderer, env_maps, name, W, H, n, 
     assert st["rays"] == cnt["rays"], (st, cnt)
     assert st["samples"] == W * H * n
     assert bit_mismatch(img, ref)[0] == 0.0
+
+
+@pytest.mark.parametrize("name", ["C3", "C4"])
+def test_split_queues_in_every_pass_match(gpu_dev_renderer, env_maps, monkeypatch, name):
+    """Split queues (a bulk pass's shadow rays traced by the any-hit wf_trace<..., 2>,
+    its continuations by <..., 1>) leave the image and the ray count unchanged whichever passes use
+    them: RT_SPLIT_KINDS=0 (one queue of both kinds in every pass), RT_SPLIT_PASSES=8 (split in
+    every secondary pass) and the default (passes 1-5) render the bulk path (frame groups of 9.4 M
+    path slots, above the finisher's budget) bit-identically, and an 8x8 window of the default
+    equals the oracle (dev library switches)."""
+    sd = cf.config_scene(name)
+    W, H, NF = 256, 144, 512
+    fp = cf.frame_params(W, H)
+    ro, frames = frames_for(fp, 1, NF)
+    out = {}
+    try:
+        for key, env in (("default", {}), ("one_queue", {"RT_SPLIT_KINDS": "0"}), ("all_passes", {"RT_SPLIT_PASSES": "8"})):
+            for k in ("RT_SPLIT_KINDS", "RT_SPLIT_PASSES"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            gpu_dev_renderer.set_max_paths(NF * W * H)  # one launch of two 256-frame groups
+            out[key] = gpu_render(gpu_dev_renderer, sd, env_maps, W, H, fp, ro)
+            assert out[key][1]["launches"] == 1 and out[key][1]["finish_steps"] == 0, out[key][1]
+    finally:
+        for k in ("RT_SPLIT_KINDS", "RT_SPLIT_PASSES"):
+            monkeypatch.delenv(k, raising=False)
+        gpu_dev_renderer.set_max_paths(0)  # the library default again (a session fixture)
+    img, st = out["default"]
+    for key in ("one_queue", "all_passes"):
+        assert out[key][1]["rays"] == st["rays"], (key, out[key][1], st)
+        assert bit_mismatch(out[key][0], img)[0] == 0.0, key
+    x0, y0 = 120, 56  # the object's silhouette region
+    ref, cnt = oracle_render(sd, env_maps, W, H, frames, x0=x0, y0=y0, w=8, h=8)
+    assert bit_mismatch(img[y0:y0 + 8, x0:x0 + 8], ref)[0] == 0.0
