@@ -48,7 +48,8 @@ phases = [
     ("gui_env_off", lambda k: ia.Input(gui={"enable_env_map": False}) if k == 0 else ia.Input()),
     ("still_after", lambda k: ia.Input()),
 ]
-s.tick(delta_time=dt, display=not a.no_display)  # first pass: allocations, code objects
+for _ in range(max(1, a.in_flight)):  # first passes: allocations (every pipeline set), code objects
+    s.tick(delta_time=dt, display=not a.no_display)
 s.flush()
 report = {"config": a.config, "width": W, "height": H, "frames_per_phase": a.frames, "frames_in_flight": a.in_flight,
           "phases": {}}
